@@ -1,0 +1,138 @@
+// oracle/ref_shim.cc -- TEST INFRASTRUCTURE ONLY.
+//
+// A thin extern "C" wrapper that is compiled together with the reference's own
+// CPU translation units *where they lie* under /root/reference (see
+// oracle/Makefile, target `ref`).  Nothing from the reference is copied into
+// this repository; this file only calls the reference's templates/functions so
+// that the pytest suite (and bench.py's cpu_baseline leg) can drive them via
+// ctypes.  The product path never loads the resulting oracle/_ref/libpszref.so.
+//
+// Wrapped reference entry points:
+//   psz::module::CPU_c_lorenzo_nd_with_outlier<f4,false,u2>::kernel   psz/src/kernel/lrz.seq.cc:35-55
+//   psz::module::CPU_x_lorenzo_nd<f4,false,u2>::kernel                psz/src/kernel/lrz.seq.cc:57-77
+//   psz::KERNEL_SEQ_{c,x}_lorenzo_{1,2,3}d1l                          psz/src/kernel/detail/lrz.seq.inl:154-545
+//   psz::module::SEQ_histogram_generic<u2>                            psz/src/kernel/hist_generic.seq.cc:17-30
+//   phf_CPU_build_canonized_codebook_v2<u2,u4>                        codec/hf/src/hf_bk.seq.cc:72-145
+//   psz::module::CPU_scatter<f4,u4>::kernel_v2                        psz/src/kernel/spvn.seq.cc:19-29
+
+#include <chrono>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+
+#include "c_type.h"
+#include "hf_impl.hh"
+#include "kernel/hist.hh"
+#include "kernel/predictor.hh"
+#include "kernel/spvn.hh"
+#include "mem/cxx_sp_cpu.h"
+
+namespace {
+using Cell = _portable::compact_cell<f4, u4>;
+}
+
+extern "C" {
+
+// Reference CPU Lorenzo compress (NOT error-bounded: no round(); BLK 256/16/8).
+// Outliers are returned in the reference's sequential append order.
+// Returns the outlier count (capacity `ol_cap` must be >= N for safety: the
+// reference kernel does not bound-check).
+uint32_t ref_c_lorenzo_f32(
+    const float* in, size_t x, size_t y, size_t z, double eb, uint16_t radius, uint16_t* codes,
+    float* ol_val, uint32_t* ol_idx, size_t ol_cap)
+{
+  auto outlier = std::make_unique<_portable::compact_CPU<f4, u4>>(ol_cap);
+  psz_len len{x, y, z};
+  psz::module::CPU_c_lorenzo_nd_with_outlier<f4, false, u2>::kernel(
+      const_cast<float*>(in), len, codes, outlier.get(), eb, radius, nullptr);
+  uint32_t n = outlier->num();
+  for (uint32_t i = 0; i < n; i++) {
+    ol_val[i] = outlier->val_idx(i).val;
+    ol_idx[i] = outlier->val_idx(i).idx;
+  }
+  return n;
+}
+
+// Reference CPU Lorenzo decompress. `out` must hold the scattered outlier
+// values and zeros elsewhere (reference convention, see lrz.seq.inl x-kernels).
+void ref_x_lorenzo_f32(
+    const uint16_t* codes, float* outlier_plane, float* out, size_t x, size_t y, size_t z,
+    double eb, uint16_t radius)
+{
+  psz_len len{x, y, z};
+  psz::module::CPU_x_lorenzo_nd<f4, false, u2>::kernel(
+      const_cast<uint16_t*>(codes), outlier_plane, out, len, eb, radius, nullptr);
+}
+
+void ref_scatter_f32(const float* val, const uint32_t* idx, uint32_t n, float* out)
+{
+  auto cells = std::make_unique<Cell[]>(n ? n : 1);
+  for (uint32_t i = 0; i < n; i++) cells[i] = Cell{val[i], idx[i]};
+  psz::module::CPU_scatter<f4, u4>::kernel_v2(cells.get(), (int)n, out);
+}
+
+void ref_histogram_u2(const uint16_t* codes, size_t n, uint32_t* hist, uint16_t bklen)
+{
+  memset(hist, 0, sizeof(uint32_t) * bklen);
+  psz::module::SEQ_histogram_generic<u2>(const_cast<uint16_t*>(codes), n, hist, bklen, nullptr);
+}
+
+// book: u32[bklen]; revbook: 4*64 + 2*bklen bytes (u2 symbols)
+int ref_build_codebook_u2(const uint32_t* hist, int bklen, uint32_t* book, uint8_t* revbook)
+{
+  int rvbk_bytes = (int)phf_reverse_book_bytes(bklen, 4, sizeof(u2));
+  memset(revbook, 0, rvbk_bytes);
+  try {
+    phf_CPU_build_canonized_codebook_v2<u2, u4>(
+        const_cast<uint32_t*>(hist), bklen, book, revbook, rvbk_bytes, nullptr);
+  }
+  catch (...) {
+    return -1;
+  }
+  return rvbk_bytes;
+}
+
+// Timing helper for the CPU baseline leg: reference CPU compress stages on a
+// 3D field, single thread.  Returns milliseconds per stage in ms[0..3]:
+// c_lorenzo, histogram, codebook, x_lorenzo.
+void ref_time_stages_f32(
+    const float* in, size_t x, size_t y, size_t z, double eb, uint16_t radius, double* ms)
+{
+  size_t n = x * y * z;
+  auto codes = std::make_unique<uint16_t[]>(n);
+  auto outlier = std::make_unique<_portable::compact_CPU<f4, u4>>(n);
+  auto hist = std::make_unique<uint32_t[]>(2 * radius);
+  auto book = std::make_unique<uint32_t[]>(2 * radius);
+  int rvbk_bytes = (int)phf_reverse_book_bytes(2 * radius, 4, sizeof(u2));
+  auto revbook = std::make_unique<uint8_t[]>(rvbk_bytes);
+  auto xdata = std::make_unique<float[]>(n);
+  psz_len len{x, y, z};
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point t0) {
+    return std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+  };
+
+  auto t0 = clk::now();
+  psz::module::CPU_c_lorenzo_nd_with_outlier<f4, false, u2>::kernel(
+      const_cast<float*>(in), len, codes.get(), outlier.get(), eb, radius, nullptr);
+  ms[0] = ms_since(t0);
+
+  memset(hist.get(), 0, sizeof(uint32_t) * 2 * radius);
+  t0 = clk::now();
+  psz::module::SEQ_histogram_generic<u2>(codes.get(), n, hist.get(), 2 * radius, nullptr);
+  ms[1] = ms_since(t0);
+
+  t0 = clk::now();
+  phf_CPU_build_canonized_codebook_v2<u2, u4>(
+      hist.get(), 2 * radius, book.get(), revbook.get(), rvbk_bytes, nullptr);
+  ms[2] = ms_since(t0);
+
+  memset(xdata.get(), 0, sizeof(float) * n);
+  psz::module::CPU_scatter<f4, u4>::kernel_v2(outlier->val_idx(), outlier->num(), xdata.get());
+  t0 = clk::now();
+  psz::module::CPU_x_lorenzo_nd<f4, false, u2>::kernel(
+      codes.get(), xdata.get(), xdata.get(), len, eb, radius, nullptr);
+  ms[3] = ms_since(t0);
+}
+
+}  // extern "C"
