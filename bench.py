@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident compress+decompress throughput of cusz_amd on MI355X.
+
+Metric (BASELINE.json): "device-resident compress+decompress GB/s (input bytes),
+512^3 f32 abs eb=1e-4".  One step = psz_compress_float + psz_decompress_float of one
+512^3 f32 field already resident in HBM (config 2 of BASELINE.json: Lorenzo-3D + histogram
++ Huffman), through the C-ABI.  value = (bytes of input processed by all ranks) / time.
+
+Multi-GPU (torchrun, one rank per GPU): every rank compresses and decompresses its own
+512^3 field (the path shards by independent fields / tile-aligned slabs, no data-path
+collective) -> "scaling": "weak"; barrier + synchronize bracket the timed steps and the
+max time over ranks is used.
+
+Extra fields on the JSON line:
+  roofline      dominant kernel: algorithmic bytes / its HIP-event duration vs 8 TB/s
+  cpu_baseline  the reference's own CPU path (compiled from /root/reference into
+                oracle/_ref; single thread) timed on this host on the same 512^3 field
+  stages_ms     per-stage device times of the last step (HIP events in the library)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--dims", default="512x512x512")
+    ap.add_argument("--eb", type=float, default=1e-4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e", action="store_true", help="also time the host-memory (PCIe) path")
+    ap.add_argument("--profile-only", action="store_true", help="few steps, no baselines (rocprof)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+
+    import cusz_amd as cz
+    from cusz_amd import datagen
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    dims = tuple(int(v) for v in args.dims.lower().split("x"))
+    dims = (dims + (1, 1))[:3]
+    n = dims[0] * dims[1] * dims[2]
+    nbytes_in = 4 * n
+
+    d_in = datagen.smooth3d_torch(dims, seed=2 + rank, device=dev)
+    d_out = torch.empty(n, dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    r = cz.Resource(cz.F4, dims, stream=stream.cuda_stream)
+    r.enable_timing(True)
+
+    def barrier():
+        if dist:
+            tdist.barrier()
+
+    def step():
+        ptr, nb, _ = r.compress(d_in.data_ptr(), args.eb, cz.Abs)
+        r.decompress(ptr, nb, d_out.data_ptr())
+        return ptr, nb
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # correctness guard on the measured configuration (error bound, every element)
+    err = (d_out.double() - d_in.double()).abs().max().item()
+    assert err <= 1.001 * args.eb, f"error bound violated: {err}"
+
+    stage_acc = np.zeros(cz.T_COUNT)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ptr, nb = step()
+        torch.cuda.synchronize()  # decompress is asynchronous; close the step
+        stage_acc += np.array(r.stage_times())
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        dt = t.item()
+    ms_per_step = 1e3 * dt / args.steps
+    value = world * nbytes_in * args.steps / dt / 1e9
+    st = stage_acc / args.steps
+    comp_ms, decomp_ms = st[cz.T_COMPRESS], st[cz.T_DECOMPRESS]
+    ratio = nbytes_in / nb
+
+    # dominant kernel roofline (algorithmic bytes per launch / event-measured duration)
+    ino = r.internals()
+    splen = r.header.splen
+    arch_bytes = nb
+    kernels = {
+        # predictor: read N*4, write codes N*2 + outlier cells 8/each
+        "lorenzo_c3d": (st[cz.T_PREDICT], 4 * n + 2 * n + 8 * splen),
+        # encoder: read codes N*2, write bitstream (archive - metadata)
+        "hf_encode": (st[cz.T_ENCODE], 2 * n + arch_bytes),
+        # decoder: read bitstream, write codes N*2
+        "hf_decode": (st[cz.T_DECODE], arch_bytes + 2 * n),
+        # reconstruct: read codes N*2 (+ sparse outlier plane), write N*4
+        "lorenzo_x3d": (st[cz.T_RECON], 2 * n + 4 * n),
+    }
+    dom = max(kernels, key=lambda k: kernels[k][0])
+    d_ms, d_bytes = kernels[dom]
+    achieved = d_bytes / (d_ms * 1e-3) / 1e9 if d_ms > 0 else None
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if os.path.exists(pmc_path):
+        try:
+            traffic = json.load(open(pmc_path)).get(dom, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1) if achieved else None,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                "traffic": traffic, "algorithmic_bytes": int(d_bytes)}
+
+    # end-to-end path from/to host memory (pinned), for DESIGN.md (never `value`)
+    e2e = None
+    if args.e2e and rank == 0:
+        h_in = d_in.cpu().pin_memory()
+        h_arch = torch.empty(nb, dtype=torch.uint8).pin_memory()
+        h_out = torch.empty(n, dtype=torch.float32).pin_memory()
+        d_arch = torch.empty(nb, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            d_in.copy_(h_in, non_blocking=True)
+            ptr, nb2, _ = r.compress(d_in.data_ptr(), args.eb, cz.Abs)
+            cz.hip_memcpy(h_arch.data_ptr(), ptr, nb2, 2)
+            d_arch[:nb2].copy_(h_arch[:nb2], non_blocking=True)
+            r.decompress(d_arch.data_ptr(), nb2, d_out.data_ptr())
+            h_out.copy_(d_out, non_blocking=True)
+            torch.cuda.synchronize()
+        e2e = round(nbytes_in * reps / (time.perf_counter() - t1) / 1e9, 2)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_only:
+        cpu = cpu_baseline(d_in, dims, args.eb, nbytes_in)
+
+    if rank == 0:
+        line = {
+            "metric": "device-resident compress+decompress GB/s (input bytes), 512³ f32 abs eb=1e-4",
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (SURVEY.md §8d config-2 field: sin/cos + 1e-3 N(0,1), seed 2+rank)",
+            "config": {"workload": f"config2: {dims[0]}x{dims[1]}x{dims[2]} f32, abs eb={args.eb}, "
+                                   "Lorenzo-3D + histogram + Huffman, compress+decompress per step",
+                       "per_rank_field_bytes": nbytes_in, "parallelism": f"dp{world} (independent fields)"},
+            "compress_gbps": round(nbytes_in / (comp_ms * 1e-3) / 1e9, 2) if comp_ms > 0 else None,
+            "decompress_gbps": round(nbytes_in / (decomp_ms * 1e-3) / 1e9, 2) if decomp_ms > 0 else None,
+            "compression_ratio": round(ratio, 3),
+            "stages_ms": {k: round(float(st[i]), 4) for k, i in
+                          [("predict", cz.T_PREDICT), ("book", cz.T_BOOK), ("encode", cz.T_ENCODE),
+                           ("finalize", cz.T_FINALIZE), ("compress", cz.T_COMPRESS),
+                           ("scatter", cz.T_SCATTER), ("decode", cz.T_DECODE), ("recon", cz.T_RECON),
+                           ("decompress", cz.T_DECOMPRESS)]},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "e2e_host_gbps": e2e,
+            "max_abs_err": err,
+        }
+        print(json.dumps(line), flush=True)
+    r.close()
+    if dist:
+        tdist.destroy_process_group()
+
+
+def cpu_baseline(d_in, dims, eb, nbytes_in):
+    """The reference CPU path (psz_seq_core) on the same field, 1 thread, this host.
+    Stages: c_lorenzo + histogram + codebook (compress; the reference has no CPU Huffman
+    encoder) and x_lorenzo (decompress; no CPU decoder).  Falls back to null if the
+    reference build (oracle/_ref) is absent."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    try:
+        import pyoracle
+    except Exception:
+        return None
+    if not pyoracle.ref_available():
+        return None
+    host = d_in.cpu().numpy()
+    try:
+        os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})
+    except Exception:
+        pass
+    t = pyoracle.ref_time_stages(host, dims, eb)
+    total_ms = t["c_lorenzo"] + t["histogram"] + t["codebook"] + t["x_lorenzo"]
+    return {"value": round(nbytes_in / (total_ms * 1e-3) / 1e9, 4), "unit": "GB/s", "cores": 1,
+            "kind": "reference",
+            "sample": f"full {dims[0]}x{dims[1]}x{dims[2]} f32 field; reference CPU path "
+                      f"(lrz.seq.cc c_lorenzo {t['c_lorenzo']:.0f} ms + hist {t['histogram']:.0f} ms + "
+                      f"codebook {t['codebook']:.2f} ms + x_lorenzo {t['x_lorenzo']:.0f} ms; "
+                      "no CPU Huffman in the reference)"}
+
+
+if __name__ == "__main__":
+    main()

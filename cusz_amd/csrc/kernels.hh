@@ -1,0 +1,101 @@
+// cusz_amd/csrc/kernels.hh -- launchers of the hand-written gfx950 kernels.
+#pragma once
+
+#include "common.hh"
+
+namespace cusz_amd {
+
+// Brick decomposition of the Lorenzo kernels (one wave64 per brick).
+struct LorenzoGeom {
+  int ndim;
+  int V;                  // elements per lane along x
+  uint32_t nbx, nby, nbz; // bricks per axis
+  uint32_t nbricks;
+  uint32_t brick_elems;   // elements per full brick
+};
+
+LorenzoGeom lorenzo_geom(int ndim, size_t lx, size_t ly, size_t lz, int elem_bytes);
+
+template <typename T>
+int launch_lorenzo_c(const T* in, size_t lx, size_t ly, size_t lz, double eb, int radius, bool zigzag,
+                     const LorenzoGeom& g, uint16_t* codes, const OutlierSink& ol, uint32_t* hist,
+                     int bklen, hipStream_t st);
+
+template <typename T>
+int launch_lorenzo_x(const uint16_t* codes, T* out, size_t lx, size_t ly, size_t lz, double eb, int radius,
+                     bool zigzag, const LorenzoGeom& g, hipStream_t st);
+
+template <typename T>
+int launch_scatter(const uint32_t* cells, size_t nnz, T* out, size_t n, hipStream_t st);
+
+// ---- Huffman (huffman.hip) ---------------------------------------------------------------
+struct HfEncodeArgs {
+  const uint16_t* codes;
+  size_t n;
+  const uint32_t* book;  // device u32[bklen]
+  int bklen;
+  int sublen;            // multiple of 256, <= 8192
+  int pardeg;
+  uint32_t* par_nbit;    // archive segment
+  uint32_t* par_entry;   // archive segment
+  uint32_t* bitstream;   // archive segment (4-byte aligned)
+  unsigned long long* status;  // pardeg/kGroup+1 lookback words, zeroed before launch
+  unsigned int* timeout;       // set nonzero if a bounded spin gave up
+};
+int launch_hf_encode(const HfEncodeArgs& a, hipStream_t st);
+
+struct HfDecodeArgs {
+  const uint32_t* bitstream;
+  const uint8_t* revbook;  // first i32[32] | entry i32[32] | keys u16[bklen]
+  int bklen;
+  const uint32_t* par_nbit;
+  const uint32_t* par_entry;
+  int sublen;
+  int pardeg;
+  size_t n;
+  uint16_t* out;
+};
+int launch_hf_decode(const HfDecodeArgs& a, hipStream_t st);
+
+// ---- pipeline glue (pipeline_kernels.hip) ---------------------------------------------------
+struct FinalizeArgs {
+  // Huffman
+  const uint32_t* par_nbit;
+  const uint32_t* par_entry;
+  int pardeg;
+  // outliers
+  const uint32_t* brick_cnt;
+  uint32_t nbricks;
+  uint32_t cap_per_brick;
+  const uint32_t* spill_cnt;
+  uint32_t spill_cap;
+  uint32_t* brick_off;  // scratch u32[nbricks+1]
+  CompressInfo* info;
+};
+int launch_finalize_scan(const FinalizeArgs& a, hipStream_t st);
+
+struct OutlierCopyArgs {
+  const uint64_t* slots;
+  const uint32_t* brick_cnt;
+  const uint32_t* brick_off;
+  uint32_t nbricks;
+  uint32_t cap_per_brick;
+  const uint64_t* spill;
+  const uint32_t* spill_cnt;
+  uint32_t spill_cap;
+  const CompressInfo* info;
+  uint8_t* archive;         // base of the archive
+  size_t bitstream_offset;  // byte offset of the bitstream (outliers follow it)
+};
+int launch_outlier_copy(const OutlierCopyArgs& a, hipStream_t st);
+
+// writes the psz_header (176 B) and phf_header (64 B + pad) with the dynamic fields filled
+int launch_write_headers(uint8_t* archive, const void* psz_hdr_tpl, const void* phf_hdr_tpl,
+                         const CompressInfo* info, size_t phf_offset, size_t bitstream_rel,
+                         hipStream_t st);
+
+// min / max (Rel mode, extrema.cuhip.inl:86-208), writes {min, max} as doubles
+template <typename T>
+int launch_extrema(const T* in, size_t n, double* d_minmax, unsigned int* d_scratch, hipStream_t st);
+
+}  // namespace cusz_amd

@@ -1,0 +1,737 @@
+// cusz_amd/csrc/lorenzo.hip -- Lorenzo predictor-quantizer and reconstructor for gfx950.
+//
+// Semantics restate the reference GPU kernels exactly (integer codes and outlier set
+// bit-exact, reconstruction in the reference's floating-point operation order):
+//   compress   psz/src/kernel/detail/lrz_c.cuhip.inl:23-109 (1D), 187-273 (2D), 275-372 (3D)
+//   decompress psz/src/kernel/detail/lrz_x.cuhip.inl:11-78 (1D), 178-269 (2D), 271-360 (3D)
+//              + scan order of psz/src/kernel/detail/wave32.cuhip.inl:7-66
+// Tiles (launch.hh:47-121): 1D 1024, 2D 32x32, 3D 8x8x8; values outside the data are 0.
+//
+// MI355X layout (not the reference's): one wave64 owns a "brick" and walks it serially,
+// each lane holding V consecutive x-elements (V=4 f32 -> 16-B loads, 1 KiB per wave
+// instruction).  3D brick = (64V) x 8 x 8: the lane keeps its 8 z-values of a row column
+// in registers, so the z-difference is in-register, the x-difference is a one-lane shuffle
+// and the y-difference uses the previous row's registers.  The code histogram is fused
+// (per-workgroup LDS bins, merged once), and outliers go to a per-brick slot, so the
+// predictor reads the input exactly once and writes only codes (+ sparse outliers).
+#include "common.hh"
+#include "kernels.hh"
+
+namespace cusz_amd {
+
+namespace {
+
+template <typename T>
+__device__ __forceinline__ T dround(T v);
+template <>
+__device__ __forceinline__ float dround<float>(float v) { return roundf(v); }
+template <>
+__device__ __forceinline__ double dround<double>(double v) { return round(v); }
+
+template <typename T>
+__device__ __forceinline__ T dabs(T v);
+template <>
+__device__ __forceinline__ float dabs<float>(float v) { return fabsf(v); }
+template <>
+__device__ __forceinline__ double dabs<double>(double v) { return fabs(v); }
+
+__device__ __forceinline__ uint16_t zz_enc(int16_t v)
+{  // composite.hh:61-70
+  return (uint16_t)(((uint16_t)v << 1) ^ (uint16_t)(v >> 15));
+}
+__device__ __forceinline__ int16_t zz_dec(uint16_t u)
+{  // composite.hh:72-83
+  return (int16_t)((u >> 1) ^ (uint16_t)(-(int16_t)(u & 1)));
+}
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
+
+// ---- vector row I/O -------------------------------------------------------------------
+template <typename T, int V>
+__device__ __forceinline__ void load_row(const T* __restrict__ p, size_t base, uint32_t x0, uint32_t lx,
+                                         bool row_ok, T (&v)[V])
+{
+  if (row_ok && x0 + V <= lx) {
+    const T* q = p + base + x0;
+    if constexpr (sizeof(T) * V == 16) {
+      auto w = *reinterpret_cast<const uint4*>(q);
+      __builtin_memcpy(&v[0], &w, 16);
+    }
+    else if constexpr (sizeof(T) * V == 8) {
+      auto w = *reinterpret_cast<const uint2*>(q);
+      __builtin_memcpy(&v[0], &w, 8);
+    }
+    else if constexpr (sizeof(T) * V == 32) {
+      auto w0 = reinterpret_cast<const uint4*>(q)[0];
+      auto w1 = reinterpret_cast<const uint4*>(q)[1];
+      __builtin_memcpy(&v[0], &w0, 16);
+      __builtin_memcpy(reinterpret_cast<char*>(&v[0]) + 16, &w1, 16);
+    }
+    else {
+#pragma unroll
+      for (int k = 0; k < V; k++) v[k] = q[k];
+    }
+  }
+  else {
+#pragma unroll
+    for (int k = 0; k < V; k++) v[k] = (row_ok && x0 + k < lx) ? p[base + x0 + k] : T(0);
+  }
+}
+
+template <int V>
+__device__ __forceinline__ void load_codes(const uint16_t* __restrict__ c, size_t base, uint32_t x0,
+                                           uint32_t lx, bool row_ok, uint16_t (&v)[V])
+{
+  if (row_ok && x0 + V <= lx) {
+    const uint16_t* q = c + base + x0;
+    if constexpr (V == 4) {
+      auto w = *reinterpret_cast<const uint2*>(q);
+      __builtin_memcpy(&v[0], &w, 8);
+    }
+    else if constexpr (V == 2) {
+      auto w = *reinterpret_cast<const uint32_t*>(q);
+      __builtin_memcpy(&v[0], &w, 4);
+    }
+    else {
+#pragma unroll
+      for (int k = 0; k < V; k++) v[k] = q[k];
+    }
+  }
+  else {
+#pragma unroll
+    for (int k = 0; k < V; k++) v[k] = (row_ok && x0 + k < lx) ? c[base + x0 + k] : uint16_t(0);
+  }
+}
+
+template <int V>
+__device__ __forceinline__ void store_codes(uint16_t* __restrict__ c, size_t base, uint32_t x0,
+                                            uint32_t lx, bool row_ok, const uint16_t (&v)[V])
+{
+  if (!row_ok) return;
+  if (x0 + V <= lx) {
+    uint16_t* q = c + base + x0;
+    if constexpr (V == 4) {
+      uint2 w;
+      __builtin_memcpy(&w, &v[0], 8);
+      *reinterpret_cast<uint2*>(q) = w;
+    }
+    else if constexpr (V == 2) {
+      uint32_t w;
+      __builtin_memcpy(&w, &v[0], 4);
+      *reinterpret_cast<uint32_t*>(q) = w;
+    }
+    else {
+#pragma unroll
+      for (int k = 0; k < V; k++) q[k] = v[k];
+    }
+  }
+  else {
+#pragma unroll
+    for (int k = 0; k < V; k++)
+      if (x0 + k < lx) c[base + x0 + k] = v[k];
+  }
+}
+
+template <typename T, int V>
+__device__ __forceinline__ void store_row(T* __restrict__ p, size_t base, uint32_t x0, uint32_t lx,
+                                          bool row_ok, const T (&v)[V])
+{
+  if (!row_ok) return;
+  if (x0 + V <= lx) {
+    T* q = p + base + x0;
+    if constexpr (sizeof(T) * V == 16) {
+      uint4 w;
+      __builtin_memcpy(&w, &v[0], 16);
+      *reinterpret_cast<uint4*>(q) = w;
+    }
+    else if constexpr (sizeof(T) * V == 8) {
+      uint2 w;
+      __builtin_memcpy(&w, &v[0], 8);
+      *reinterpret_cast<uint2*>(q) = w;
+    }
+    else if constexpr (sizeof(T) * V == 32) {
+      uint4 w0, w1;
+      __builtin_memcpy(&w0, &v[0], 16);
+      __builtin_memcpy(&w1, reinterpret_cast<const char*>(&v[0]) + 16, 16);
+      reinterpret_cast<uint4*>(q)[0] = w0;
+      reinterpret_cast<uint4*>(q)[1] = w1;
+    }
+    else {
+#pragma unroll
+      for (int k = 0; k < V; k++) q[k] = v[k];
+    }
+  }
+  else {
+#pragma unroll
+    for (int k = 0; k < V; k++)
+      if (x0 + k < lx) p[base + x0 + k] = v[k];
+  }
+}
+
+// ---- quantization + outlier/histogram side effects -------------------------------------
+// lrz_c.cuhip.inl:310-331: code = (|d| < r) ? (u2)(d + r) : 0; outlier cell {(f4)(d + r), idx}
+// (ZigZag: code = zz((i16)(q*d)), cell val (f4)d).
+template <typename T, bool ZZ>
+__device__ __forceinline__ uint16_t quantize(T d, T r, bool& ol, float& olval)
+{
+  bool q = dabs(d) < r;
+  ol = !q;
+  if constexpr (ZZ) {
+    olval = (float)d;
+    return q ? zz_enc((int16_t)(int)d) : uint16_t(0);
+  }
+  else {
+    T c = d + r;
+    olval = (float)c;
+    return q ? (uint16_t)(int)c : uint16_t(0);
+  }
+}
+
+// Emit the outliers of one wave row in (lane, k) order into the brick's slot.
+template <int V>
+__device__ __forceinline__ void emit_outliers(const OutlierSink& ol, uint32_t brick, uint32_t& cnt,
+                                              uint32_t mask, const float (&val)[V],
+                                              const size_t (&idx)[V])
+{
+  const int c = __popc(mask);
+  const uint64_t b0 = __ballot(c & 1), b1 = __ballot(c & 2), b2 = __ballot(c & 4);
+  const uint64_t lt = lanemask_lt();
+  uint32_t pos = cnt + __popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt);
+  const uint32_t tot = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+  uint64_t* slot = ol.slots + (size_t)brick * ol.cap_per_brick;
+#pragma unroll
+  for (int k = 0; k < V; k++) {
+    if ((mask >> k) & 1u) {
+      const uint64_t cell = make_cell(val[k], (uint32_t)idx[k]);
+      if (pos < ol.cap_per_brick)
+        slot[pos] = cell;
+      else {
+        uint32_t s = atomicAdd(ol.spill_cnt, 1u);
+        if (s < ol.spill_cap) ol.spill[s] = cell;
+      }
+      pos++;
+    }
+  }
+  cnt += tot;
+}
+
+// Quantize one row of V elements (in-range mask), store codes, histogram, outliers.
+template <typename T, int V, bool ZZ>
+__device__ __forceinline__ void quantize_row(const T (&d)[V], T r, uint16_t* __restrict__ codes,
+                                             size_t base, uint32_t x0, uint32_t lx, bool row_ok,
+                                             uint32_t* s_hist, const OutlierSink& ol, uint32_t brick,
+                                             uint32_t& cnt)
+{
+  uint16_t q[V];
+  float olv[V];
+  size_t idx[V];
+  uint32_t mask = 0;
+#pragma unroll
+  for (int k = 0; k < V; k++) {
+    bool is_ol;
+    q[k] = quantize<T, ZZ>(d[k], r, is_ol, olv[k]);
+    idx[k] = base + x0 + k;
+    const bool in = row_ok && (x0 + k < lx);
+    if (in) atomicAdd(&s_hist[q[k]], 1u);
+    mask |= (uint32_t)(in && is_ol) << k;
+  }
+  store_codes<V>(codes, base, x0, lx, row_ok, q);
+  if (__ballot(mask != 0)) emit_outliers<V>(ol, brick, cnt, mask, olv, idx);
+}
+
+__device__ __forceinline__ void hist_init(uint32_t* s_hist, int bklen)
+{
+  for (int i = threadIdx.x; i < bklen; i += blockDim.x) s_hist[i] = 0;
+  __syncthreads();
+}
+
+__device__ __forceinline__ void hist_flush(uint32_t* s_hist, uint32_t* g_hist, int bklen)
+{
+  __syncthreads();
+  for (int i = threadIdx.x; i < bklen; i += blockDim.x) {
+    uint32_t v = s_hist[i];
+    if (v) atomicAdd(&g_hist[i], v);
+  }
+}
+
+// Hillis-Steele step of the reference's shuffle scans (val += shfl_up(val, D) when the
+// in-tile position >= D), for a lane holding V consecutive positions of a TW-wide tile.
+template <typename T, int V, int TW, int D>
+__device__ __forceinline__ void hs_step(T (&t)[V], uint32_t x0)
+{
+  T old[V];
+#pragma unroll
+  for (int k = 0; k < V; k++) old[k] = t[k];
+#pragma unroll
+  for (int k = 0; k < V; k++) {
+    constexpr int dummy = 0;
+    (void)dummy;
+    const int kk = k - D;
+    T src;
+    if (kk >= 0)
+      src = old[kk >= 0 ? kk : 0];
+    else {
+      const int L = (-kk + V - 1) / V;
+      const int k2 = kk + L * V;
+      src = __shfl_up(old[k2], L);
+    }
+    const uint32_t px = (x0 + k) % TW;
+    if (px >= (uint32_t)D) t[k] = old[k] + src;
+  }
+}
+
+}  // namespace
+
+// =========================================================================================
+// predictor-quantizer kernels
+// =========================================================================================
+
+// 1D: brick = 16 tiles of 1024; wave step = 256 elements (V=4 per lane).
+template <typename T, bool ZZ>
+__global__ void __launch_bounds__(256)
+k_lorenzo_c1d(const T* __restrict__ in, size_t n, T ebx2_r, T r, uint16_t* __restrict__ codes,
+              OutlierSink ol, uint32_t* __restrict__ g_hist, int bklen, uint32_t nbricks)
+{
+  constexpr int V = 4;
+  __shared__ uint32_t s_hist[kMaxBklen];
+  hist_init(s_hist, bklen);
+  const int lane = threadIdx.x & 63;
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  for (uint32_t brick = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); brick < nbricks; brick += nw) {
+    uint32_t cnt = 0;
+    T carry = 0;
+    const size_t bbase = (size_t)brick * 16384;
+    for (int s = 0; s < 64; s++) {
+      const size_t base = bbase + (size_t)s * 256;
+      // treat [base, n) as one long row of length n - base
+      const uint32_t rowlen = (uint32_t)(n - base < 256 ? n - base : 256);
+      const uint32_t x0 = lane * V;
+      if (base >= n) break;
+      T p[V];
+      load_row<T, V>(in, base, x0, rowlen, true, p);
+#pragma unroll
+      for (int k = 0; k < V; k++) p[k] = dround(p[k] * ebx2_r);
+      T west = __shfl_up(p[V - 1], 1);
+      const T last = __shfl(p[V - 1], 63);
+      if (lane == 0) west = (s & 3) ? carry : T(0);
+      carry = last;
+      T d[V];
+#pragma unroll
+      for (int k = V - 1; k > 0; k--) d[k] = p[k] - p[k - 1];
+      d[0] = p[0] - west;
+      quantize_row<T, V, ZZ>(d, r, codes, base, x0, rowlen, true, s_hist, ol, brick, cnt);
+    }
+    if (lane == 0) ol.brick_cnt[brick] = cnt;
+  }
+  hist_flush(s_hist, g_hist, bklen);
+}
+
+// 2D: brick = (64V) x 32 rows (one tile row); tiles 32 wide.
+template <typename T, int V, bool ZZ>
+__global__ void __launch_bounds__(256)
+k_lorenzo_c2d(const T* __restrict__ in, uint32_t lx, uint32_t ly, T ebx2_r, T r,
+              uint16_t* __restrict__ codes, OutlierSink ol, uint32_t* __restrict__ g_hist, int bklen,
+              uint32_t nbx, uint32_t nbricks)
+{
+  __shared__ uint32_t s_hist[kMaxBklen];
+  hist_init(s_hist, bklen);
+  const int lane = threadIdx.x & 63;
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  for (uint32_t brick = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); brick < nbricks; brick += nw) {
+    const uint32_t bx = brick % nbx, by = brick / nbx;
+    const uint32_t x0 = bx * (64 * V) + lane * V, y0 = by * 32;
+    uint32_t cnt = 0;
+    T pprev[V];
+#pragma unroll
+    for (int k = 0; k < V; k++) pprev[k] = 0;
+    for (int y = 0; y < 32; y++) {
+      const uint32_t gy = y0 + y;
+      const bool ok = gy < ly;
+      if (!__ballot(ok)) break;
+      const size_t base = (size_t)gy * lx;
+      T p[V];
+      load_row<T, V>(in, base, x0, lx, ok, p);
+#pragma unroll
+      for (int k = 0; k < V; k++) p[k] = dround(p[k] * ebx2_r);
+      T a[V];
+#pragma unroll
+      for (int k = 0; k < V; k++) a[k] = p[k] - pprev[k], pprev[k] = p[k];
+      const T west = __shfl_up(a[V - 1], 1);
+      T d[V];
+#pragma unroll
+      for (int k = V - 1; k > 0; k--) d[k] = a[k] - a[k - 1];
+      d[0] = (x0 % 32 != 0) ? a[0] - west : a[0];
+      quantize_row<T, V, ZZ>(d, r, codes, base, x0, lx, ok, s_hist, ol, brick, cnt);
+    }
+    if (lane == 0) ol.brick_cnt[brick] = cnt;
+  }
+  hist_flush(s_hist, g_hist, bklen);
+}
+
+// 3D: brick = (64V) x 8 x 8 (8V tiles of 8^3 along x).
+template <typename T, int V, bool ZZ>
+__global__ void __launch_bounds__(256)
+k_lorenzo_c3d(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T ebx2_r, T r,
+              uint16_t* __restrict__ codes, OutlierSink ol, uint32_t* __restrict__ g_hist, int bklen,
+              uint32_t nbx, uint32_t nby, uint32_t nbricks)
+{
+  __shared__ uint32_t s_hist[kMaxBklen];
+  hist_init(s_hist, bklen);
+  const int lane = threadIdx.x & 63;
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  const size_t plane = (size_t)lx * ly;
+  for (uint32_t brick = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); brick < nbricks; brick += nw) {
+    const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
+    const uint32_t x0 = bx * (64 * V) + lane * V, y0 = by * 8, z0 = bz * 8;
+    uint32_t cnt = 0;
+    T bprev[8][V];
+    for (int y = 0; y < 8; y++) {
+      const uint32_t gy = y0 + y;
+      if (gy >= ly) break;
+      T p[8][V];
+#pragma unroll
+      for (int z = 0; z < 8; z++) {
+        const bool ok = (z0 + z) < lz;
+        load_row<T, V>(in, (size_t)(z0 + z) * plane + (size_t)gy * lx, x0, lx, ok, p[z]);
+#pragma unroll
+        for (int k = 0; k < V; k++) p[z][k] = dround(p[z][k] * ebx2_r);
+      }
+      // z-difference (descending keeps p[z-1] original); a[0] = p[0] - 0
+#pragma unroll
+      for (int z = 7; z > 0; z--)
+#pragma unroll
+        for (int k = 0; k < V; k++) p[z][k] = p[z][k] - p[z - 1][k];
+      // x-difference inside 8-wide tiles
+#pragma unroll
+      for (int z = 0; z < 8; z++) {
+        const T west = __shfl_up(p[z][V - 1], 1);
+#pragma unroll
+        for (int k = V - 1; k > 0; k--) p[z][k] = p[z][k] - p[z][k - 1];
+        if (x0 % 8 != 0) p[z][0] = p[z][0] - west;
+      }
+      // y-difference against the previous row of the brick
+#pragma unroll
+      for (int z = 0; z < 8; z++) {
+        T d[V];
+#pragma unroll
+        for (int k = 0; k < V; k++) {
+          d[k] = (y > 0) ? p[z][k] - bprev[z][k] : p[z][k];
+          bprev[z][k] = p[z][k];
+        }
+        const bool ok = (z0 + z) < lz;
+        quantize_row<T, V, ZZ>(d, r, codes, (size_t)(z0 + z) * plane + (size_t)gy * lx, x0, lx, ok,
+                               s_hist, ol, brick, cnt);
+      }
+    }
+    if (lane == 0) ol.brick_cnt[brick] = cnt;
+  }
+  hist_flush(s_hist, g_hist, bklen);
+}
+
+// =========================================================================================
+// reconstruct kernels.  `out` doubles as the outlier plane: the scatter kernel wrote the
+// outlier values there; it is read only where code == 0, so non-outlier positions need not
+// be pre-zeroed (Lorenzo).  ZigZag additionally needs a zeroed plane (code 0 = delta 0).
+// =========================================================================================
+
+template <typename T, int V, bool ZZ>
+__device__ __forceinline__ void fuse_row(const uint16_t* __restrict__ codes, const T* plane, size_t base,
+                                         uint32_t x0, uint32_t lx, bool ok, T r, T (&v)[V])
+{
+  uint16_t c[V];
+  load_codes<V>(codes, base, x0, lx, ok, c);
+#pragma unroll
+  for (int k = 0; k < V; k++) {
+    const bool in = ok && (x0 + k < lx);
+    T o = 0;
+    if (in && c[k] == 0) o = plane[base + x0 + k];
+    if constexpr (ZZ)
+      v[k] = in ? o + (T)zz_dec(c[k]) : T(0);
+    else
+      v[k] = in ? (o + (T)c[k]) - r : T(0);
+  }
+}
+
+template <typename T, bool ZZ>
+__global__ void __launch_bounds__(256)
+k_lorenzo_x1d(const uint16_t* __restrict__ codes, T* out, size_t n, T ebx2, T r, uint32_t nbricks)
+{
+  constexpr int V = 4;  // the reference thread owns 4 consecutive elements (launch.hh:124-132)
+  const int lane = threadIdx.x & 63;
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  for (uint32_t brick = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); brick < nbricks; brick += nw) {
+    const size_t bbase = (size_t)brick * 16384;
+    T carry = 0;
+    for (int s = 0; s < 64; s++) {
+      const size_t base = bbase + (size_t)s * 256;
+      if (base >= n) break;
+      const uint32_t rowlen = (uint32_t)(n - base < 256 ? n - base : 256);
+      const uint32_t x0 = lane * V;
+      T b[V];
+      fuse_row<T, V, ZZ>(codes, out, base, x0, rowlen, true, r, b);
+      // per-thread sequential scan (wave32.cuhip.inl:10)
+#pragma unroll
+      for (int k = 1; k < V; k++) b[k] = b[k] + b[k - 1];
+      // 32-lane Hillis-Steele over thread totals (wave32.cuhip.inl:14-17)
+      T addend = b[V - 1];
+#pragma unroll
+      for (int d = 1; d < 32; d *= 2) {
+        T nb = __shfl_up(addend, d, 32);
+        if ((lane & 31) >= d) addend = addend + nb;
+      }
+      const T prev = __shfl_up(addend, 1, 32);
+      if ((lane & 31) > 0)
+#pragma unroll
+        for (int k = 0; k < V; k++) b[k] = b[k] + prev;
+      // cross-warp serial exclusive scan over the tile's 8 warps (wave32.cuhip.inl:38-42)
+      const T tot0 = __shfl(b[V - 1], 31), tot1 = __shfl(b[V - 1], 63);
+      if ((s & 3) == 0) carry = 0;
+      const T c0 = carry, c1 = c0 + tot0;
+      const T add = lane < 32 ? c0 : c1;
+#pragma unroll
+      for (int k = 0; k < V; k++) b[k] = (b[k] + add) * ebx2;
+      carry = c1 + tot1;
+      store_row<T, V>(out, base, x0, rowlen, true, b);
+    }
+  }
+}
+
+template <typename T, int V, bool ZZ>
+__global__ void __launch_bounds__(256)
+k_lorenzo_x2d(const uint16_t* __restrict__ codes, T* out, uint32_t lx, uint32_t ly, T ebx2, T r,
+              uint32_t nbx, uint32_t nbricks)
+{
+  const int lane = threadIdx.x & 63;
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  for (uint32_t brick = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); brick < nbricks; brick += nw) {
+    const uint32_t bx = brick % nbx, by = brick / nbx;
+    const uint32_t x0 = bx * (64 * V) + lane * V, y0 = by * 32;
+    T s[V], S0[V], acc1[V], acc2[V];
+    for (int y = 0; y < 32; y++) {
+      const uint32_t gy = y0 + y;
+      const bool ok = gy < ly;
+      if (!__ballot(ok)) break;
+      const size_t base = (size_t)gy * lx;
+      T v[V];
+      fuse_row<T, V, ZZ>(codes, out, base, x0, lx, ok, r, v);
+      const int strip = y >> 3;
+      T t[V];
+#pragma unroll
+      for (int k = 0; k < V; k++) {
+        s[k] = (y & 7) ? v[k] + s[k] : v[k];  // per-strip sequential scan (lrz_x:214)
+        if (strip == 0)
+          t[k] = s[k];
+        else if (strip == 1)
+          t[k] = s[k] + S0[k];
+        else if (strip == 2)
+          t[k] = s[k] + acc1[k];
+        else
+          t[k] = s[k] + acc2[k];
+        if ((y & 7) == 7) {  // strip totals -> cross-strip addends (lrz_x:217-236)
+          if (strip == 0) S0[k] = s[k];
+          if (strip == 1) acc1[k] = s[k] + S0[k];
+          if (strip == 2) acc2[k] = s[k] + acc1[k];
+        }
+      }
+      // 32-wide Hillis-Steele along x (lrz_x:247-253)
+      hs_step<T, V, 32, 1>(t, x0);
+      hs_step<T, V, 32, 2>(t, x0);
+      hs_step<T, V, 32, 4>(t, x0);
+      hs_step<T, V, 32, 8>(t, x0);
+      hs_step<T, V, 32, 16>(t, x0);
+#pragma unroll
+      for (int k = 0; k < V; k++) t[k] = t[k] * ebx2;
+      store_row<T, V>(out, base, x0, lx, ok, t);
+    }
+  }
+}
+
+template <typename T, int V, bool ZZ>
+__global__ void __launch_bounds__(256)
+k_lorenzo_x3d(const uint16_t* __restrict__ codes, T* out, uint32_t lx, uint32_t ly, uint32_t lz, T ebx2,
+              T r, uint32_t nbx, uint32_t nby, uint32_t nbricks)
+{
+  const int lane = threadIdx.x & 63;
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  const size_t plane = (size_t)lx * ly;
+  for (uint32_t brick = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); brick < nbricks; brick += nw) {
+    const uint32_t bx = brick % nbx, tt = brick / nbx, by = tt % nby, bz = tt / nby;
+    const uint32_t x0 = bx * (64 * V) + lane * V, y0 = by * 8, z0 = bz * 8;
+    T s[8][V];
+    for (int y = 0; y < 8; y++) {
+      const uint32_t gy = y0 + y;
+      if (gy >= ly) break;
+      T t[8][V];
+#pragma unroll
+      for (int z = 0; z < 8; z++) {
+        const bool ok = (z0 + z) < lz;
+        T v[V];
+        fuse_row<T, V, ZZ>(codes, out, (size_t)(z0 + z) * plane + (size_t)gy * lx, x0, lx, ok, r, v);
+#pragma unroll
+        for (int k = 0; k < V; k++) {
+          s[z][k] = (y > 0) ? v[k] + s[z][k] : v[k];  // y sequential (lrz_x:315)
+          t[z][k] = s[z][k];
+        }
+      }
+      // x Hillis-Steele within 8-wide tiles (lrz_x:324-327)
+#pragma unroll
+      for (int z = 0; z < 8; z++) {
+        hs_step<T, V, 8, 1>(t[z], x0);
+        hs_step<T, V, 8, 2>(t[z], x0);
+        hs_step<T, V, 8, 4>(t[z], x0);
+      }
+      // z Hillis-Steele (lrz_x:335-338), in-lane; descending z keeps sources unmodified
+#pragma unroll
+      for (int d = 1; d < 8; d *= 2)
+#pragma unroll
+        for (int z = 7; z >= d; z--)
+#pragma unroll
+          for (int k = 0; k < V; k++) t[z][k] = t[z][k] + t[z - d][k];
+#pragma unroll
+      for (int z = 0; z < 8; z++) {
+#pragma unroll
+        for (int k = 0; k < V; k++) t[z][k] = t[z][k] * ebx2;
+        store_row<T, V>(out, (size_t)(z0 + z) * plane + (size_t)gy * lx, x0, lx, (z0 + z) < lz, t[z]);
+      }
+    }
+  }
+}
+
+// outlier scatter (spvn.cuhip.inl:41-50): cells are {f32 val, u32 idx}, 4-byte aligned in
+// the archive (read as two u32).
+template <typename T>
+__global__ void __launch_bounds__(256)
+k_scatter(const uint32_t* __restrict__ cells, size_t nnz, T* out, size_t n)
+{
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nnz; i += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t vb = cells[2 * i], idx = cells[2 * i + 1];
+    if (idx < n) out[idx] = (T)__builtin_bit_cast(float, vb);
+  }
+}
+
+// =========================================================================================
+// host launchers
+// =========================================================================================
+
+static inline uint32_t cdiv(size_t a, size_t b) { return (uint32_t)((a + b - 1) / b); }
+
+static int grid_for(uint32_t nbricks)
+{
+  const uint32_t waves = nbricks;
+  uint32_t g = (waves + 3) / 4;
+  return (int)(g < 4096 ? (g ? g : 1) : 4096);
+}
+
+LorenzoGeom lorenzo_geom(int ndim, size_t lx, size_t ly, size_t lz, int elem_bytes)
+{
+  LorenzoGeom g{};
+  g.ndim = ndim;
+  if (ndim == 1) {
+    g.V = 4;
+    g.nbx = cdiv(lx * ly * lz, 16384), g.nby = 1, g.nbz = 1;
+    g.brick_elems = 16384;
+  }
+  else {
+    int V = 1;
+    if (elem_bytes == 4 && lx % 4 == 0) V = 4;
+    else if (elem_bytes == 8 && lx % 2 == 0) V = 2;
+    else if (elem_bytes == 4 && lx % 2 == 0) V = 2;
+    g.V = V;
+    g.nbx = cdiv(lx, 64 * V);
+    if (ndim == 2) g.nby = cdiv(ly, 32), g.nbz = 1, g.brick_elems = 64 * V * 32;
+    else g.nby = cdiv(ly, 8), g.nbz = cdiv(lz, 8), g.brick_elems = 64 * V * 64;
+  }
+  g.nbricks = g.nbx * g.nby * g.nbz;
+  return g;
+}
+
+#define DISPATCH_V(V, ...)                       \
+  switch (V) {                                   \
+    case 4: { constexpr int VV = 4; __VA_ARGS__; } break; \
+    case 2: { constexpr int VV = 2; __VA_ARGS__; } break; \
+    default: { constexpr int VV = 1; __VA_ARGS__; } break; \
+  }
+
+template <typename T>
+int launch_lorenzo_c(const T* in, size_t lx, size_t ly, size_t lz, double eb, int radius, bool zigzag,
+                     const LorenzoGeom& g, uint16_t* codes, const OutlierSink& ol, uint32_t* hist,
+                     int bklen, hipStream_t st)
+{
+  const T ebx2_r = (T)(1.0 / (eb * 2));  // lrz_c.cuhip.inl:489
+  const T r = (T)radius;
+  const int grid = grid_for(g.nbricks);
+  if (g.ndim == 1) {
+    if (zigzag)
+      k_lorenzo_c1d<T, true><<<grid, 256, 0, st>>>(in, lx, ebx2_r, r, codes, ol, hist, bklen, g.nbricks);
+    else
+      k_lorenzo_c1d<T, false><<<grid, 256, 0, st>>>(in, lx, ebx2_r, r, codes, ol, hist, bklen, g.nbricks);
+  }
+  else if (g.ndim == 2) {
+    DISPATCH_V(g.V, if (zigzag) k_lorenzo_c2d<T, VV, true><<<grid, 256, 0, st>>>(
+                        in, lx, ly, ebx2_r, r, codes, ol, hist, bklen, g.nbx, g.nbricks);
+               else k_lorenzo_c2d<T, VV, false><<<grid, 256, 0, st>>>(
+                   in, lx, ly, ebx2_r, r, codes, ol, hist, bklen, g.nbx, g.nbricks));
+  }
+  else {
+    DISPATCH_V(g.V, if (zigzag) k_lorenzo_c3d<T, VV, true><<<grid, 256, 0, st>>>(
+                        in, lx, ly, lz, ebx2_r, r, codes, ol, hist, bklen, g.nbx, g.nby, g.nbricks);
+               else k_lorenzo_c3d<T, VV, false><<<grid, 256, 0, st>>>(
+                   in, lx, ly, lz, ebx2_r, r, codes, ol, hist, bklen, g.nbx, g.nby, g.nbricks));
+  }
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+int launch_lorenzo_x(const uint16_t* codes, T* out, size_t lx, size_t ly, size_t lz, double eb, int radius,
+                     bool zigzag, const LorenzoGeom& g, hipStream_t st)
+{
+  const T ebx2 = (T)(eb * 2);  // lrz_x.cuhip.inl:432
+  const T r = (T)radius;
+  const int grid = grid_for(g.nbricks);
+  if (g.ndim == 1) {
+    if (zigzag)
+      k_lorenzo_x1d<T, true><<<grid, 256, 0, st>>>(codes, out, lx, ebx2, r, g.nbricks);
+    else
+      k_lorenzo_x1d<T, false><<<grid, 256, 0, st>>>(codes, out, lx, ebx2, r, g.nbricks);
+  }
+  else if (g.ndim == 2) {
+    DISPATCH_V(g.V, if (zigzag) k_lorenzo_x2d<T, VV, true><<<grid, 256, 0, st>>>(
+                        codes, out, lx, ly, ebx2, r, g.nbx, g.nbricks);
+               else k_lorenzo_x2d<T, VV, false><<<grid, 256, 0, st>>>(codes, out, lx, ly, ebx2, r,
+                                                                        g.nbx, g.nbricks));
+  }
+  else {
+    DISPATCH_V(g.V, if (zigzag) k_lorenzo_x3d<T, VV, true><<<grid, 256, 0, st>>>(
+                        codes, out, lx, ly, lz, ebx2, r, g.nbx, g.nby, g.nbricks);
+               else k_lorenzo_x3d<T, VV, false><<<grid, 256, 0, st>>>(
+                   codes, out, lx, ly, lz, ebx2, r, g.nbx, g.nby, g.nbricks));
+  }
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+int launch_scatter(const uint32_t* cells, size_t nnz, T* out, size_t n, hipStream_t st)
+{
+  if (nnz == 0) return 0;
+  uint32_t grid = cdiv(nnz, 256);
+  if (grid > 4096) grid = 4096;
+  k_scatter<T><<<grid, 256, 0, st>>>(cells, nnz, out, n);
+  return (int)hipGetLastError();
+}
+
+template int launch_lorenzo_c<float>(const float*, size_t, size_t, size_t, double, int, bool,
+                                     const LorenzoGeom&, uint16_t*, const OutlierSink&, uint32_t*, int,
+                                     hipStream_t);
+template int launch_lorenzo_c<double>(const double*, size_t, size_t, size_t, double, int, bool,
+                                      const LorenzoGeom&, uint16_t*, const OutlierSink&, uint32_t*, int,
+                                      hipStream_t);
+template int launch_lorenzo_x<float>(const uint16_t*, float*, size_t, size_t, size_t, double, int, bool,
+                                     const LorenzoGeom&, hipStream_t);
+template int launch_lorenzo_x<double>(const uint16_t*, double*, size_t, size_t, size_t, double, int, bool,
+                                      const LorenzoGeom&, hipStream_t);
+template int launch_scatter<float>(const uint32_t*, size_t, float*, size_t, hipStream_t);
+template int launch_scatter<double>(const uint32_t*, size_t, double*, size_t, hipStream_t);
+
+}  // namespace cusz_amd

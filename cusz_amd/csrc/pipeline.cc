@@ -1,0 +1,620 @@
+// cusz_amd/csrc/pipeline.cc -- the compression pipeline behind the cuSZ C API.
+//
+// Replaces psz::compression_pipeline<T,u2> (psz/src/compressor.inl:268-529) and the C-API
+// glue of psz/src/libcusz.cc:219-366.  One device-resident Pipeline per psz_resource:
+//
+//   compress:  [extrema (Rel)] -> predict+quantize+histogram+outliers (1 kernel)
+//              -> histogram D2H, host codebook, book/revbook H2D (the one host round trip
+//                 the reference algorithm needs: the codebook depends on the full histogram)
+//              -> Huffman encode straight into the archive (1 kernel, device look-back)
+//              -> finalize: outlier compaction + headers written on device
+//              -> one 176-B header read-back (compress is synchronous, as in the reference)
+//   decompress: outlier scatter -> Huffman decode -> Lorenzo reconstruct (queued, no sync)
+//
+// The reference does 5+ host round trips per compress and copies a 2N-byte buffer
+// (SURVEY.md §3.1); here the archive is assembled in place.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+
+#include "common.hh"
+#include "cusz.h"
+#include "cusz_amd.h"
+#include "cusz_rev1.h"
+#include "hf.h"
+#include "kernels.hh"
+
+namespace cusz_amd {
+
+int build_codebook(const uint32_t* hist, int bklen, uint32_t* book, uint8_t* revbook);
+int hf_encode_groups(int sublen, int pardeg);
+
+int report_hip_error(hipError_t e, const char* expr, const char* file, int line)
+{
+  std::fprintf(stderr, "[cusz_amd] HIP error %d (%s) at %s:%d: %s\n", (int)e, hipGetErrorString(e), file, line,
+               expr);
+  return PSZ_ABORT_NOT_IMPLEMENTED;  // closest psz_error_status for a runtime failure
+}
+
+static int ndim_of(psz_len l)
+{  // launch.hh:19-28
+  if (l.z == 1 && l.y == 1) return 1;
+  if (l.z == 1) return 2;
+  return 3;
+}
+
+static void tune_chunking(size_t n, int device, int* sublen, int* pardeg)
+{  // libphf.cc:26-70, evaluated on the caller's device (reference forces device 0)
+  int ncu = 256, maxthr = 1024;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 256;
+  if (hipDeviceGetAttribute(&maxthr, hipDeviceAttributeMaxThreadsPerBlock, device) != hipSuccess) maxthr = 1024;
+  const size_t nthread = (size_t)maxthr * (size_t)ncu / 4;
+  size_t s = (std::max<size_t>(n, 1) - 1) / nthread + 1;
+  s = ((s - 1) / 256 + 1) * 256;
+  if (s > 8192) s = 8192;  // encoder limit (LDS cell buffer); format allows any sublen
+  *sublen = (int)s;
+  *pardeg = (int)((std::max<size_t>(n, 1) - 1) / s + 1);
+}
+
+struct Pipeline {
+  psz_dtype dtype;
+  psz_len len;
+  size_t n = 0;
+  int ndim = 1;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int elem_bytes = 4;
+
+  LorenzoGeom geom{};
+  int sublen = 256, pardeg = 1;
+  int user_sublen = 0;
+  uint32_t cap_per_brick = 0, spill_cap = 0;
+  size_t splen = 0;
+
+  // device
+  uint16_t* d_codes = nullptr;
+  uint32_t* d_hist = nullptr;
+  uint32_t* d_book = nullptr;
+  uint64_t* d_slots = nullptr;
+  uint32_t* d_brick_cnt = nullptr;
+  uint32_t* d_brick_off = nullptr;
+  uint64_t* d_spill = nullptr;
+  uint8_t* d_small = nullptr;  // spill_cnt | timeout | info | minmax | extrema scratch
+  unsigned long long* d_status = nullptr;
+  size_t status_words = 0;
+  uint8_t* d_archive = nullptr;
+  size_t archive_cap = 0;
+
+  // pinned host
+  uint32_t* h_hist = nullptr;
+  uint32_t* h_book = nullptr;
+  uint8_t* h_revbook = nullptr;
+  uint8_t* h_readback = nullptr;  // psz_header | CompressInfo | minmax
+
+  bool timing = false;
+  hipEvent_t ev[12] = {};
+  float stage_ms[PSZ_AMD_T_COUNT] = {0};
+
+  uint32_t* spill_cnt() { return reinterpret_cast<uint32_t*>(d_small); }
+  unsigned int* timeout() { return reinterpret_cast<unsigned int*>(d_small + 16); }
+  CompressInfo* info() { return reinterpret_cast<CompressInfo*>(d_small + 64); }
+  double* minmax() { return reinterpret_cast<double*>(d_small + 256); }
+  unsigned int* ext_scratch() { return reinterpret_cast<unsigned int*>(d_small + 512); }
+  static constexpr size_t kSmallBytes = 512 + 2 * 1024 * 8;
+
+  ~Pipeline() { release(); }
+
+  void release()
+  {
+    for (void* p : {(void*)d_codes, (void*)d_hist, (void*)d_book, (void*)d_slots, (void*)d_brick_cnt,
+                    (void*)d_brick_off, (void*)d_spill, (void*)d_small, (void*)d_status, (void*)d_archive})
+      if (p) (void)hipFree(p);
+    for (void* p : {(void*)h_hist, (void*)h_book, (void*)h_revbook, (void*)h_readback})
+      if (p) (void)hipHostFree(p);
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e), e = nullptr;
+    d_codes = nullptr, d_hist = nullptr, d_book = nullptr, d_slots = nullptr, d_brick_cnt = nullptr;
+    d_brick_off = nullptr, d_spill = nullptr, d_small = nullptr, d_status = nullptr, d_archive = nullptr;
+    h_hist = nullptr, h_book = nullptr, h_revbook = nullptr, h_readback = nullptr;
+  }
+
+  size_t rvbk_bytes(int bklen) const { return 4 * 64 + 2 * (size_t)bklen; }
+
+  size_t bitstream_cells_cap() const { return (n * kLmax + 31) / 32 + (size_t)pardeg + 8; }
+
+  int init(psz_dtype dt, psz_len l, void* st)
+  {
+    dtype = dt;
+    len = l;
+    if (l.x == 0 || l.y == 0 || l.z == 0) return PSZ_ABORT_UNSUPPORTED_DIMENSION;
+    n = l.x * l.y * l.z;
+    if (n >= (1ull << 32)) return PSZ_ABORT_UNSUPPORTED_DIMENSION;  // u32 outlier index (sp_interface.h)
+    ndim = ndim_of(l);
+    elem_bytes = dt == F8 ? 8 : 4;
+    stream = (hipStream_t)st;
+    CUSZ_AMD_HIP_CHECK(hipGetDevice(&device));
+    tune_chunking(n, device, &sublen, &pardeg);
+    geom = lorenzo_geom(ndim, l.x, l.y, l.z, elem_bytes);
+    // outlier capacity: 10 % of the input like the reference (buf_comp.hh:55), as per-brick
+    // slots plus an equally large spill list for bricks above 10 %.
+    cap_per_brick = geom.brick_elems / 10 + 16;
+    spill_cap = (uint32_t)(n / 10 + 1024);
+
+    CUSZ_AMD_HIP_CHECK(hipMalloc(&d_codes, (n + 64) * sizeof(uint16_t)));
+    CUSZ_AMD_HIP_CHECK(hipMalloc(&d_hist, kMaxBklen * sizeof(uint32_t)));
+    CUSZ_AMD_HIP_CHECK(hipMalloc(&d_book, kMaxBklen * sizeof(uint32_t)));
+    CUSZ_AMD_HIP_CHECK(hipMalloc(&d_slots, (size_t)geom.nbricks * cap_per_brick * 8));
+    CUSZ_AMD_HIP_CHECK(hipMalloc(&d_brick_cnt, (size_t)geom.nbricks * 4));
+    CUSZ_AMD_HIP_CHECK(hipMalloc(&d_brick_off, ((size_t)geom.nbricks + 1) * 4));
+    CUSZ_AMD_HIP_CHECK(hipMalloc(&d_spill, (size_t)spill_cap * 8));
+    CUSZ_AMD_HIP_CHECK(hipMalloc(&d_small, kSmallBytes));
+    CUSZ_AMD_HIP_CHECK(hipMemset(d_small, 0, kSmallBytes));
+    CUSZ_AMD_HIP_CHECK(alloc_chunk_state());
+    CUSZ_AMD_HIP_CHECK(hipHostMalloc(&h_hist, kMaxBklen * 4, hipHostMallocDefault));
+    CUSZ_AMD_HIP_CHECK(hipHostMalloc(&h_book, kMaxBklen * 4, hipHostMallocDefault));
+    CUSZ_AMD_HIP_CHECK(hipHostMalloc(&h_revbook, 4 * 64 + 2 * kMaxBklen, hipHostMallocDefault));
+    CUSZ_AMD_HIP_CHECK(hipHostMalloc(&h_readback, 1024, hipHostMallocDefault));
+    for (auto& e : ev) CUSZ_AMD_HIP_CHECK(hipEventCreate(&e));
+    return PSZ_SUCCESS;
+  }
+
+  hipError_t alloc_chunk_state()
+  {
+    if (d_status) (void)hipFree(d_status), d_status = nullptr;
+    if (d_archive) (void)hipFree(d_archive), d_archive = nullptr;
+    status_words = (size_t)hf_encode_groups(sublen, pardeg) + 1;
+    hipError_t e = hipMalloc(&d_status, status_words * 8);
+    if (e != hipSuccess) return e;
+    archive_cap = 176 + 128 + rvbk_bytes(kMaxBklen) + 8 * (size_t)pardeg + 4 * bitstream_cells_cap() +
+                  8 * ((size_t)geom.nbricks * cap_per_brick + spill_cap) + 64;
+    return hipMalloc(&d_archive, archive_cap);
+  }
+
+  void mark(int i)
+  {
+    if (timing) (void)hipEventRecord(ev[i], stream);
+  }
+
+  float span(int a, int b)
+  {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, ev[a], ev[b]) != hipSuccess) ms = -1;
+    return ms;
+  }
+
+  template <typename T>
+  int compress(psz_header* h, const T* in, uint8_t** out, size_t* outlen)
+  {
+    const psz_predictor pred = h->pipeline.predictor;
+    if (pred != Lorenzo && pred != LorenzoZigZag) return PSZ_ABORT_NO_SUCH_PREDICTOR;
+    if (h->pipeline.codec1 != Huffman) return PSZ_ABORT_NO_SUCH_CODEC;
+    const bool zz = pred == LorenzoZigZag;
+    const int radius = h->rc.radius;
+    const int bklen = 2 * radius;
+    if (radius < 1 || bklen > kMaxBklen) return PSZ_ABORT_NOT_IMPLEMENTED;
+
+    if (user_sublen) {
+      int s = std::min(8192, ((user_sublen + 255) / 256) * 256);
+      if (s != sublen) {
+        sublen = s;
+        pardeg = (int)((n - 1) / s + 1);
+        CUSZ_AMD_HIP_CHECK(alloc_chunk_state());
+      }
+    }
+
+    mark(0);
+    // Rel mode: eb *= (max - min)  (libcusz.cc:287-293; range in double of T extrema)
+    if (h->rc.mode == Rel) {
+      CUSZ_AMD_HIP_CHECK((hipError_t)launch_extrema<T>(in, n, minmax(), ext_scratch(), stream));
+      CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(h_readback + 512, minmax(), 16, hipMemcpyDeviceToHost, stream));
+      CUSZ_AMD_HIP_CHECK(hipStreamSynchronize(stream));
+      double mm[2];
+      std::memcpy(mm, h_readback + 512, 16);
+      h->min_val = mm[0], h->max_val = mm[1];
+      h->rc.eb *= (mm[1] - mm[0]);
+    }
+    const double eb = h->rc.eb;
+
+    // per-call state reset (the reference never resets these: SURVEY.md Appendix B.3)
+    CUSZ_AMD_HIP_CHECK(hipMemsetAsync(d_hist, 0, (size_t)bklen * 4, stream));
+    CUSZ_AMD_HIP_CHECK(hipMemsetAsync(d_small, 0, 64, stream));
+    CUSZ_AMD_HIP_CHECK(hipMemsetAsync(d_status, 0, status_words * 8, stream));
+    mark(1);
+
+    OutlierSink ol{d_slots, d_brick_cnt, d_spill, spill_cnt(), cap_per_brick, spill_cap};
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_lorenzo_c<T>(in, len.x, len.y, len.z, eb, radius, zz, geom, d_codes,
+                                                       ol, d_hist, bklen, stream));
+    mark(2);
+
+    // codebook on the host (hf_hl.cc:21-34), one round trip
+    CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(h_hist, d_hist, (size_t)bklen * 4, hipMemcpyDeviceToHost, stream));
+    CUSZ_AMD_HIP_CHECK(hipStreamSynchronize(stream));
+    const int rv = build_codebook(h_hist, bklen, h_book, h_revbook);
+    const size_t phf_off = 176;  // + anchor bytes (0 for Lorenzo)
+    const size_t rvbk = (size_t)rv;
+    const size_t nbit_rel = 128 + rvbk, entry_rel = nbit_rel + 4 * (size_t)pardeg;
+    const size_t bits_rel = entry_rel + 4 * (size_t)pardeg;
+    CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(d_book, h_book, (size_t)bklen * 4, hipMemcpyHostToDevice, stream));
+    CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(d_archive + phf_off + 128, h_revbook, rvbk, hipMemcpyHostToDevice, stream));
+    mark(3);
+
+    HfEncodeArgs ea{d_codes,
+                    n,
+                    d_book,
+                    bklen,
+                    sublen,
+                    pardeg,
+                    reinterpret_cast<uint32_t*>(d_archive + phf_off + nbit_rel),
+                    reinterpret_cast<uint32_t*>(d_archive + phf_off + entry_rel),
+                    reinterpret_cast<uint32_t*>(d_archive + phf_off + bits_rel),
+                    d_status,
+                    timeout()};
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_hf_encode(ea, stream));
+    mark(4);
+
+    FinalizeArgs fa{ea.par_nbit, ea.par_entry, pardeg, d_brick_cnt, geom.nbricks, cap_per_brick,
+                    spill_cnt(),  spill_cap,     d_brick_off, info()};
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_finalize_scan(fa, stream));
+    OutlierCopyArgs oa{d_slots, d_brick_cnt, d_brick_off, geom.nbricks, cap_per_brick, d_spill,
+                       spill_cnt(), spill_cap, info(), d_archive, phf_off + bits_rel};
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_outlier_copy(oa, stream));
+
+    // header templates: static fields from the host, dynamic ones filled on the device
+    h->vle_sublen = sublen;
+    h->vle_pardeg = pardeg;
+    h->len = len;
+    h->entry[0] = 0, h->entry[1] = 176, h->entry[2] = (uint32_t)phf_off;
+    phf_header ph;
+    std::memset(&ph, 0, sizeof(ph));
+    ph.bklen = bklen, ph.sublen = sublen, ph.pardeg = pardeg, ph.original_len = n;
+    ph.entry[0] = 0, ph.entry[1] = 128, ph.entry[2] = (uint32_t)nbit_rel, ph.entry[3] = (uint32_t)entry_rel;
+    ph.entry[4] = (uint32_t)bits_rel;
+    CUSZ_AMD_HIP_CHECK(
+        (hipError_t)launch_write_headers(d_archive, h, &ph, info(), phf_off, bits_rel, stream));
+    CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(h_readback, d_archive, 176, hipMemcpyDeviceToHost, stream));
+    CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(h_readback + 256, info(), sizeof(CompressInfo), hipMemcpyDeviceToHost, stream));
+    CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(h_readback + 384, timeout(), 4, hipMemcpyDeviceToHost, stream));
+    mark(5);
+    CUSZ_AMD_HIP_CHECK(hipStreamSynchronize(stream));
+
+    CompressInfo ci;
+    std::memcpy(&ci, h_readback + 256, sizeof(ci));
+    unsigned int tmo;
+    std::memcpy(&tmo, h_readback + 384, 4);
+    std::memcpy(h, h_readback, 176);
+    splen = (size_t)ci.splen;
+    if (timing) {
+      stage_ms[PSZ_AMD_T_EXTREMA] = span(0, 1);
+      stage_ms[PSZ_AMD_T_PREDICT] = span(1, 2);
+      stage_ms[PSZ_AMD_T_BOOK] = span(2, 3);
+      stage_ms[PSZ_AMD_T_ENCODE] = span(3, 4);
+      stage_ms[PSZ_AMD_T_FINALIZE] = span(4, 5);
+      stage_ms[PSZ_AMD_T_COMPRESS] = span(0, 5);
+    }
+    if (tmo) {
+      std::fprintf(stderr, "[cusz_amd] encoder look-back timed out\n");
+      return PSZ_ABORT_NOT_IMPLEMENTED;
+    }
+    if (ci.outlier_lost) return PSZ_WARN_OUTLIER_TOO_MANY;
+    *out = d_archive;
+    *outlen = h->entry[PSZHEADER_ENC_PASS2_END];
+    return PSZ_SUCCESS;
+  }
+
+  int decode_codes(const psz_header* h, const uint8_t* in)
+  {
+    const int bklen = 2 * h->rc.radius;
+    const size_t phf_off = h->entry[PSZHEADER_ENCODED];
+    const size_t rvbk = rvbk_bytes(bklen);
+    const int pd = h->vle_pardeg, sl = h->vle_sublen;
+    const uint8_t* phf = in + phf_off;
+    HfDecodeArgs da{reinterpret_cast<const uint32_t*>(phf + 128 + rvbk + 8 * (size_t)pd),
+                    phf + 128,
+                    bklen,
+                    reinterpret_cast<const uint32_t*>(phf + 128 + rvbk),
+                    reinterpret_cast<const uint32_t*>(phf + 128 + rvbk + 4 * (size_t)pd),
+                    sl,
+                    pd,
+                    n,
+                    d_codes};
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_hf_decode(da, stream));
+    return PSZ_SUCCESS;
+  }
+
+  template <typename T>
+  int decompress(const psz_header* h, const uint8_t* in, T* out)
+  {
+    const psz_predictor pred = h->pipeline.predictor;
+    if (pred != Lorenzo && pred != LorenzoZigZag) return PSZ_ABORT_NO_SUCH_PREDICTOR;
+    const bool zz = pred == LorenzoZigZag;
+    if (h->len.x != len.x || h->len.y != len.y || h->len.z != len.z) return PSZ_ABORT_UNSUPPORTED_DIMENSION;
+    mark(6);
+    if (zz) CUSZ_AMD_HIP_CHECK(hipMemsetAsync(out, 0, n * sizeof(T), stream));
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_scatter<T>(
+        reinterpret_cast<const uint32_t*>(in + h->entry[PSZHEADER_SPFMT]), h->splen, out, n, stream));
+    mark(7);
+    int s = decode_codes(h, in);
+    if (s) return s;
+    mark(8);
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_lorenzo_x<T>(d_codes, out, len.x, len.y, len.z, h->rc.eb, h->rc.radius,
+                                                       zz, geom, stream));
+    mark(9);
+    return PSZ_SUCCESS;
+  }
+
+  void collect_decompress_times()
+  {
+    if (!timing) return;
+    (void)hipEventSynchronize(ev[9]);
+    stage_ms[PSZ_AMD_T_SCATTER] = span(6, 7);
+    stage_ms[PSZ_AMD_T_DECODE] = span(7, 8);
+    stage_ms[PSZ_AMD_T_RECON] = span(8, 9);
+    stage_ms[PSZ_AMD_T_DECOMPRESS] = span(6, 9);
+  }
+};
+
+static Pipeline* P(psz_resource* m) { return m ? reinterpret_cast<Pipeline*>(m->buf) : nullptr; }
+
+}  // namespace cusz_amd
+
+using cusz_amd::Pipeline;
+
+// =========================================================================================
+// resource-manager API (cusz_rev1.h)
+// =========================================================================================
+
+static psz_resource* make_resource(psz_header* hdr, void* stream)
+{
+  auto* m = new (std::nothrow) psz_resource;
+  if (!m) return nullptr;
+  std::memset(m, 0, sizeof(*m));
+  m->header = hdr;
+  m->len_linear = hdr->len.x * hdr->len.y * hdr->len.z;
+  m->stream = stream;
+  m->device = AMDGPU;
+  m->dict_size = (uint16_t)(hdr->rc.radius * 2);
+  auto* p = new (std::nothrow) Pipeline;
+  if (!p) {
+    delete m;
+    return nullptr;
+  }
+  int st = p->init(hdr->dtype, hdr->len, stream);
+  m->buf = p;
+  m->ndim = p->ndim;
+  m->last_error = (psz_error_status)st;
+  if (st != PSZ_SUCCESS) {
+    delete p;
+    delete hdr;
+    delete m;
+    return nullptr;
+  }
+  return m;
+}
+
+extern "C" {
+
+psz_resource* psz_create_resource_manager(psz_dtype dtype, psz_len len, psz_pipeline pipeline, void* stream)
+{
+  if (dtype != F4 && dtype != F8) return nullptr;
+  auto* h = new (std::nothrow) psz_header;
+  if (!h) return nullptr;
+  std::memset(h, 0, sizeof(*h));
+  h->dtype = dtype;
+  h->pipeline = pipeline;
+  h->len = len;
+  h->rc.radius = DEFAULT_RADIUS;
+  h->intp_param = make_default_params();
+  auto* m = make_resource(h, stream);
+  if (m) phf_coarse_tune(m->len_linear, &h->vle_sublen, &h->vle_pardeg);
+  return m;
+}
+
+psz_resource* psz_create_resource_manager_from_header(psz_header* header, void* stream)
+{
+  if (!header || (header->dtype != F4 && header->dtype != F8)) return nullptr;
+  auto* h = new (std::nothrow) psz_header;
+  if (!h) return nullptr;
+  std::memcpy(h, header, sizeof(psz_header));
+  return make_resource(h, stream);
+}
+
+void psz_modify_resource_manager_from_header(psz_resource* m, psz_header* header)
+{
+  if (!m || !header) return;
+  std::memcpy(m->header, header, sizeof(psz_header));
+  m->dict_size = (uint16_t)(m->header->rc.radius * 2);
+  m->len_linear = header->len.x * header->len.y * header->len.z;
+}
+
+int psz_release_resource(psz_resource* m)
+{
+  if (!m) return PSZ_SUCCESS;
+  delete cusz_amd::P(m);
+  delete m->cli;
+  delete m->header;
+  delete m;
+  return PSZ_SUCCESS;
+}
+
+}  // extern "C"
+
+template <typename T>
+static int compress_impl(psz_resource* m, psz_rc2 rc, T* in, psz_header* out_h, uint8_t** out, size_t* outlen)
+{
+  if (!m || !in || !out || !outlen) return PSZ_ABORT_NOT_IMPLEMENTED;
+  Pipeline* p = cusz_amd::P(m);
+  if ((sizeof(T) == 4) != (m->header->dtype == F4)) return PSZ_ABORT_UNSUPPORTED_TYPE;
+  int status = PSZ_SUCCESS;
+  if (rc.radius > 512) rc.radius = 512, status = PSZ_WARN_RADIUS_TOO_LARGE;  // libcusz.cc:281-285
+  m->header->rc = rc;
+  m->header->user_input_eb = rc.eb;
+  m->dict_size = (uint16_t)(rc.radius * 2);
+  int s = p->compress<T>(m->header, in, out, outlen);
+  if (out_h) *out_h = *m->header;
+  return s != PSZ_SUCCESS ? s : status;
+}
+
+extern "C" {
+
+int psz_compress_float(psz_resource* m, psz_rc2 rc, float* in, psz_header* out_h, uint8_t** out, size_t* outlen)
+{
+  return compress_impl<float>(m, rc, in, out_h, out, outlen);
+}
+
+int psz_compress_double(psz_resource* m, psz_rc2 rc, double* in, psz_header* out_h, uint8_t** out,
+                        size_t* outlen)
+{
+  return compress_impl<double>(m, rc, in, out_h, out, outlen);
+}
+
+int psz_compress_analyize_float(psz_resource* m, psz_rc2 rc, float* in, u4* exported_h_hist)
+{
+  // compressor.inl:305-337: predict + histogram, export the histogram to the host
+  uint8_t* dummy;
+  size_t bytes;
+  int s = compress_impl<float>(m, rc, in, nullptr, &dummy, &bytes);
+  if (s != PSZ_SUCCESS && s != PSZ_WARN_RADIUS_TOO_LARGE) return s;
+  Pipeline* p = cusz_amd::P(m);
+  std::memcpy(exported_h_hist, p->h_hist, sizeof(u4) * 2 * m->header->rc.radius);
+  return s;
+}
+
+}  // extern "C"
+
+template <typename T>
+static int decompress_impl(psz_resource* m, uint8_t* in, size_t in_len, T* out)
+{
+  if (!m || !in || !out) return PSZ_ABORT_NOT_IMPLEMENTED;
+  (void)in_len;
+  Pipeline* p = cusz_amd::P(m);
+  if ((sizeof(T) == 4) != (m->header->dtype == F4)) return PSZ_ABORT_UNSUPPORTED_TYPE;
+  int s = p->decompress<T>(m->header, in, out);
+  if (s == PSZ_SUCCESS && p->timing) p->collect_decompress_times();
+  return s;
+}
+
+extern "C" {
+
+int psz_decompress_float(psz_resource* m, uint8_t* in, size_t const in_len, float* out)
+{
+  return decompress_impl<float>(m, in, in_len, out);
+}
+
+int psz_decompress_double(psz_resource* m, uint8_t* in, size_t const in_len, double* out)
+{
+  return decompress_impl<double>(m, in, in_len, out);
+}
+
+// =========================================================================================
+// extensions (cusz_amd.h)
+// =========================================================================================
+
+int psz_amd_get_internals(psz_resource* m, psz_amd_internals* o)
+{
+  Pipeline* p = cusz_amd::P(m);
+  if (!p || !o) return PSZ_ABORT_NOT_IMPLEMENTED;
+  o->d_quant_codes = p->d_codes;
+  o->d_hist = p->d_hist;
+  o->d_book = p->d_book;
+  o->len = p->n;
+  o->bklen = 2 * m->header->rc.radius;
+  o->sublen = p->sublen;
+  o->pardeg = p->pardeg;
+  o->ndim = p->ndim;
+  o->splen = p->splen;
+  o->archive_capacity = p->archive_cap;
+  return PSZ_SUCCESS;
+}
+
+int psz_amd_enable_timing(psz_resource* m, int on)
+{
+  Pipeline* p = cusz_amd::P(m);
+  if (!p) return PSZ_ABORT_NOT_IMPLEMENTED;
+  p->timing = on != 0;
+  return PSZ_SUCCESS;
+}
+
+int psz_amd_stage_times(psz_resource* m, float* ms, int n)
+{
+  Pipeline* p = cusz_amd::P(m);
+  if (!p || !ms) return PSZ_ABORT_NOT_IMPLEMENTED;
+  for (int i = 0; i < n && i < PSZ_AMD_T_COUNT; i++) ms[i] = p->stage_ms[i];
+  return PSZ_SUCCESS;
+}
+
+int psz_amd_set_sublen(psz_resource* m, int sublen)
+{
+  Pipeline* p = cusz_amd::P(m);
+  if (!p || sublen < 0) return PSZ_ABORT_NOT_IMPLEMENTED;
+  p->user_sublen = sublen;
+  if (sublen == 0) {
+    cusz_amd::tune_chunking(p->n, p->device, &p->sublen, &p->pardeg);
+    if (p->alloc_chunk_state() != hipSuccess) return PSZ_ABORT_NOT_IMPLEMENTED;
+  }
+  return PSZ_SUCCESS;
+}
+
+int psz_amd_decode_codes(psz_resource* m, uint8_t* in)
+{
+  Pipeline* p = cusz_amd::P(m);
+  if (!p || !in) return PSZ_ABORT_NOT_IMPLEMENTED;
+  return p->decode_codes(m->header, in);
+}
+
+const char* psz_amd_version(void) { return "cusz_amd 0.1 (gfx950)"; }
+
+// internal: the older API passes a stream per call (cusz.h psz_compress/psz_decompress)
+int cusz_amd_set_stream(psz_resource* m, void* stream)
+{
+  Pipeline* p = cusz_amd::P(m);
+  if (!p) return PSZ_ABORT_NOT_IMPLEMENTED;
+  p->stream = (hipStream_t)stream;
+  m->stream = stream;
+  return PSZ_SUCCESS;
+}
+
+// =========================================================================================
+// header / phf helpers (psz/src/utils/header.c:9-30, codec/hf/src/libphf.cc:26-76)
+// =========================================================================================
+
+psz_len pszheader_len(psz_header* h) { return h->len; }
+size_t pszheader_len_linear(psz_header* h) { return h->len.x * h->len.y * h->len.z; }
+size_t pszheader_segments(psz_header* h)
+{
+  (void)h;
+  return sizeof(psz_header);
+}
+size_t pszheader_filesize(psz_header* h) { return h->entry[PSZHEADER_ENC_PASS2_END]; }
+size_t pszheader_uncompressed_len(psz_header* h) { return pszheader_len_linear(h); }
+size_t pszheader_compressed_bytes(psz_header* h) { return pszheader_filesize(h); }
+
+uint32_t phf_encoded_bytes(phf_header* h) { return h->entry[PHFHEADER_END]; }
+
+size_t phf_coarse_tune_sublen(size_t len)
+{
+  int dev = 0, s, p;
+  (void)hipGetDevice(&dev);
+  cusz_amd::tune_chunking(len, dev, &s, &p);
+  return (size_t)s;
+}
+
+void phf_coarse_tune(size_t len, int* sublen, int* pardeg)
+{
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  cusz_amd::tune_chunking(len, dev, sublen, pardeg);
+}
+
+size_t phf_reverse_book_bytes(u2 bklen, size_t BK_UNIT_BYTES, size_t SYM_BYTES)
+{
+  return BK_UNIT_BYTES * (2 * BK_UNIT_BYTES * 8) + SYM_BYTES * bklen;
+}
+
+void phf_version(void) { std::printf("\n///  cusz_amd HF (gfx950) build\n"); }
+void phf_versioninfo(void) { phf_version(); }
+
+}  // extern "C"

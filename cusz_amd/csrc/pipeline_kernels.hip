@@ -1,0 +1,212 @@
+// cusz_amd/csrc/pipeline_kernels.hip -- small device-side glue of the compress pipeline:
+// archive finalisation (segment sizes, outlier compaction, headers) and the Rel-mode
+// extrema probe.  Everything stays on the device; the host reads back one header at the end.
+//
+// Reference counterparts: compress wrap-up psz/src/compressor.inl:398-418 (D2D concat),
+// phf header/offsets codec/hf/src/hf_buf.cc:191-211, GPU_extrema
+// psz/src/stat/detail/extrema.cuhip.inl:86-208.
+#include "common.hh"
+#include "kernels.hh"
+
+namespace cusz_amd {
+
+namespace {
+
+__device__ __forceinline__ unsigned long long wsum64(unsigned long long v)
+{
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d);
+  return v;
+}
+
+// one workgroup of 1024 threads
+__global__ void __launch_bounds__(1024) k_finalize_scan(FinalizeArgs a)
+{
+  __shared__ unsigned long long s_red[16];
+  __shared__ uint32_t s_scan[16];
+  __shared__ uint32_t s_carry;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+
+  // total bits = sum(par_nbit)
+  unsigned long long acc = 0;
+  for (int i = tid; i < a.pardeg; i += 1024) acc += a.par_nbit[i];
+  acc = wsum64(acc);
+  if (lane == 0) s_red[wid] = acc;
+  if (tid == 0) s_carry = 0;
+  __syncthreads();
+
+  // exclusive scan of per-brick outlier counts (clamped to the slot capacity)
+  for (uint32_t base = 0; base < a.nbricks; base += 1024) {
+    const uint32_t b = base + tid;
+    const uint32_t v = b < a.nbricks ? min(a.brick_cnt[b], a.cap_per_brick) : 0u;
+    uint32_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      uint32_t t = __shfl_up(inc, d);
+      if (lane >= d) inc += t;
+    }
+    if (lane == 63) s_scan[wid] = inc;
+    __syncthreads();
+    uint32_t off = s_carry;
+    for (int w = 0; w < wid; w++) off += s_scan[w];
+    if (b < a.nbricks) a.brick_off[b] = off + inc - v;
+    __syncthreads();
+    if (tid == 1023) s_carry = off + inc;
+    __syncthreads();
+  }
+
+  if (tid == 0) {
+    unsigned long long tb = 0;
+    for (int w = 0; w < 16; w++) tb += s_red[w];
+    const int last = a.pardeg - 1;
+    const unsigned long long ncell =
+        last >= 0 ? (unsigned long long)a.par_entry[last] + ((a.par_nbit[last] + 31u) >> 5) : 0ull;
+    const uint32_t slot_total = s_carry;
+    const uint32_t sp = *a.spill_cnt;
+    const uint32_t sp_kept = sp < a.spill_cap ? sp : a.spill_cap;
+    unsigned long long clamped = 0;  // cells beyond a full slot always went to the spill list
+    a.brick_off[a.nbricks] = slot_total;
+    a.info->total_nbit = tb;
+    a.info->total_ncell = ncell;
+    a.info->splen = (unsigned long long)slot_total + sp_kept;
+    a.info->outlier_lost = (sp > a.spill_cap ? sp - a.spill_cap : 0u) + clamped;
+  }
+}
+
+// one wave per brick copies its slot to the archive; trailing blocks copy the spill list
+__global__ void __launch_bounds__(256) k_outlier_copy(OutlierCopyArgs a, uint32_t spill_blocks)
+{
+  const unsigned long long ncell = a.info->total_ncell;
+  uint32_t* dst = reinterpret_cast<uint32_t*>(a.archive + a.bitstream_offset + ncell * 4);
+  const uint32_t slot_total = a.brick_off[a.nbricks];
+  const uint32_t brick_blocks = gridDim.x - spill_blocks;
+  if (blockIdx.x < brick_blocks) {
+    const uint32_t brick = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (brick >= a.nbricks) return;
+    const uint32_t cnt = min(a.brick_cnt[brick], a.cap_per_brick);
+    const uint64_t* src = a.slots + (size_t)brick * a.cap_per_brick;
+    uint32_t* d = dst + 2ull * a.brick_off[brick];
+    for (uint32_t i = threadIdx.x & 63; i < cnt; i += 64) {
+      const uint64_t c = src[i];
+      d[2 * i] = (uint32_t)c;
+      d[2 * i + 1] = (uint32_t)(c >> 32);
+    }
+  }
+  else {
+    const uint32_t sp = min(*a.spill_cnt, a.spill_cap);
+    uint32_t* d = dst + 2ull * slot_total;
+    for (uint32_t i = (blockIdx.x - brick_blocks) * 256 + threadIdx.x; i < sp; i += spill_blocks * 256) {
+      const uint64_t c = a.spill[i];
+      d[2 * i] = (uint32_t)c;
+      d[2 * i + 1] = (uint32_t)(c >> 32);
+    }
+  }
+}
+
+struct HeaderTpl {
+  uint32_t psz[176 / 4];
+  uint32_t phf[64 / 4];
+};
+
+__global__ void k_write_headers(uint8_t* archive, HeaderTpl t, const CompressInfo* info, size_t phf_offset,
+                                size_t bitstream_rel)
+{
+  if (threadIdx.x != 0) return;
+  // phf header (hf.h:40-46): total_nbit @24, total_ncell @32, entry[6] @40
+  uint32_t* phf = t.phf;
+  const unsigned long long nb = info->total_nbit, nc = info->total_ncell, sp = info->splen;
+  phf[6] = (uint32_t)nb, phf[7] = (uint32_t)(nb >> 32);
+  phf[8] = (uint32_t)nc, phf[9] = (uint32_t)(nc >> 32);
+  const uint32_t phf_end = (uint32_t)(bitstream_rel + nc * 4);
+  phf[10 + 5] = phf_end;  // entry[END]; entries 0..4 are static, set by the host
+  // psz header (header.h:19-48): entry[6] @56, splen @104
+  uint32_t* psz = t.psz;
+  const uint32_t e_spfmt = (uint32_t)(phf_offset + phf_end);
+  psz[14 + 3] = e_spfmt;
+  psz[14 + 4] = (uint32_t)(e_spfmt + sp * 8);
+  psz[14 + 5] = (uint32_t)(e_spfmt + sp * 8);
+  psz[26] = (uint32_t)sp, psz[27] = (uint32_t)(sp >> 32);
+  uint32_t* a32 = reinterpret_cast<uint32_t*>(archive);
+  for (int i = 0; i < 176 / 4; i++) a32[i] = psz[i];
+  uint32_t* p32 = reinterpret_cast<uint32_t*>(archive + phf_offset);
+  for (int i = 0; i < 64 / 4; i++) p32[i] = phf[i];
+  for (int i = 64 / 4; i < 128 / 4; i++) p32[i] = 0;  // defined padding (reference: stale)
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_extrema_partial(const T* __restrict__ in, size_t n, double* part)
+{
+  __shared__ T s_mn[4], s_mx[4];
+  T mn = INFINITY, mx = -INFINITY;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const T v = in[i];
+    mn = v < mn ? v : mn;
+    mx = v > mx ? v : mx;
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    T a = __shfl_xor(mn, d), b = __shfl_xor(mx, d);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) s_mn[wid] = mn, s_mx[wid] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; w++) mn = s_mn[w] < mn ? s_mn[w] : mn, mx = s_mx[w] > mx ? s_mx[w] : mx;
+    part[2 * blockIdx.x] = (double)s_mn[0] < (double)mn ? (double)s_mn[0] : (double)mn;
+    part[2 * blockIdx.x + 1] = (double)s_mx[0] > (double)mx ? (double)s_mx[0] : (double)mx;
+  }
+}
+
+__global__ void k_extrema_final(const double* part, int nparts, double* out)
+{
+  if (threadIdx.x != 0) return;
+  double mn = INFINITY, mx = -INFINITY;
+  for (int i = 0; i < nparts; i++) mn = part[2 * i] < mn ? part[2 * i] : mn, mx = part[2 * i + 1] > mx ? part[2 * i + 1] : mx;
+  out[0] = mn, out[1] = mx;
+}
+
+}  // namespace
+
+int launch_finalize_scan(const FinalizeArgs& a, hipStream_t st)
+{
+  k_finalize_scan<<<1, 1024, 0, st>>>(a);
+  return (int)hipGetLastError();
+}
+
+int launch_outlier_copy(const OutlierCopyArgs& a, hipStream_t st)
+{
+  const uint32_t brick_blocks = (a.nbricks + 3) / 4;
+  const uint32_t spill_blocks = 64;
+  k_outlier_copy<<<brick_blocks + spill_blocks, 256, 0, st>>>(a, spill_blocks);
+  return (int)hipGetLastError();
+}
+
+int launch_write_headers(uint8_t* archive, const void* psz_hdr_tpl, const void* phf_hdr_tpl,
+                         const CompressInfo* info, size_t phf_offset, size_t bitstream_rel, hipStream_t st)
+{
+  HeaderTpl t;
+  __builtin_memcpy(t.psz, psz_hdr_tpl, 176);
+  __builtin_memcpy(t.phf, phf_hdr_tpl, 64);
+  k_write_headers<<<1, 64, 0, st>>>(archive, t, info, phf_offset, bitstream_rel);
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+int launch_extrema(const T* in, size_t n, double* d_minmax, unsigned int* d_scratch, hipStream_t st)
+{
+  // d_scratch must hold 2 * 1024 doubles of partials
+  double* part = reinterpret_cast<double*>(d_scratch);
+  int grid = (int)((n + 255) / 256);
+  if (grid > 1024) grid = 1024;
+  if (grid < 1) grid = 1;
+  k_extrema_partial<T><<<grid, 256, 0, st>>>(in, n, part);
+  k_extrema_final<<<1, 64, 0, st>>>(part, grid, d_minmax);
+  return (int)hipGetLastError();
+}
+
+template int launch_extrema<float>(const float*, size_t, double*, unsigned int*, hipStream_t);
+template int launch_extrema<double>(const double*, size_t, double*, unsigned int*, hipStream_t);
+
+}  // namespace cusz_amd

@@ -1,0 +1,67 @@
+/* include/cusz_amd.h -- extensions of this implementation beyond the cuSZ C API.
+ *
+ * None of these exist in the reference; they expose what the MI355X build measures and
+ * what the parity tests need (stage timings, intermediate device buffers, tuning knobs,
+ * slab sharding helpers for multi-GPU runs).  All functions return psz_error_status codes.
+ */
+#ifndef CUSZ_AMD_EXT_H
+#define CUSZ_AMD_EXT_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "cusz/context.h"
+
+/* Stage indices for psz_amd_stage_times (milliseconds of the last call, HIP events on the
+ * manager's stream; only filled after psz_amd_enable_timing(m, 1)). */
+enum {
+  PSZ_AMD_T_EXTREMA = 0,   /* Rel mode range probe                         */
+  PSZ_AMD_T_PREDICT = 1,   /* Lorenzo predict-quantize + histogram + outliers */
+  PSZ_AMD_T_BOOK = 2,      /* histogram D2H + host codebook + H2D          */
+  PSZ_AMD_T_ENCODE = 3,    /* Huffman encode (bit packing + look-back)      */
+  PSZ_AMD_T_FINALIZE = 4,  /* outlier compaction + headers + readback       */
+  PSZ_AMD_T_COMPRESS = 5,  /* whole compress call                           */
+  PSZ_AMD_T_SCATTER = 6,   /* decompress: outlier scatter (+ zeroing)       */
+  PSZ_AMD_T_DECODE = 7,    /* decompress: Huffman decode                    */
+  PSZ_AMD_T_RECON = 8,     /* decompress: Lorenzo reconstruct               */
+  PSZ_AMD_T_DECOMPRESS = 9,/* whole decompress call                         */
+  PSZ_AMD_T_COUNT = 10
+};
+
+typedef struct psz_amd_internals {
+  uint16_t* d_quant_codes; /* quant codes of the last compress (or decoded codes) */
+  uint32_t* d_hist;        /* histogram u32[bklen] of the last compress          */
+  uint32_t* d_book;        /* codebook u32[bklen]                                 */
+  size_t len;              /* number of elements                                  */
+  int bklen;
+  int sublen;
+  int pardeg;
+  int ndim;
+  size_t splen;            /* outlier cells of the last compress                  */
+  size_t archive_capacity; /* bytes reserved for the device archive               */
+} psz_amd_internals;
+
+int psz_amd_get_internals(psz_resource* m, psz_amd_internals* out);
+int psz_amd_enable_timing(psz_resource* m, int on);
+int psz_amd_stage_times(psz_resource* m, float* ms, int n);
+
+/* Override the Huffman chunk length (symbols per chunk, rounded up to a multiple of 256,
+ * at most 8192) used by the next compress; 0 restores cuSZ's tuning rule
+ * (libphf.cc:26-70 evaluated on the current device). */
+int psz_amd_set_sublen(psz_resource* m, int sublen);
+
+/* Decode-only entry point used by the multi-GPU gather path and tests: decodes the Huffman
+ * segment of a device archive into the manager's code buffer. */
+int psz_amd_decode_codes(psz_resource* m, uint8_t* IN_d_compressed);
+
+const char* psz_amd_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CUSZ_AMD_EXT_H */

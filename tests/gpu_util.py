@@ -1,0 +1,68 @@
+"""Device-memory helpers for the GPU tests (torch for allocation, hip runtime for copies)."""
+import ctypes as C
+
+import numpy as np
+
+_hip = None
+
+
+def hip():
+    global _hip
+    if _hip is None:
+        _hip = C.CDLL("libamdhip64.so")
+        _hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        _hip.hipMemcpy.restype = C.c_int
+        _hip.hipDeviceSynchronize.restype = C.c_int
+    return _hip
+
+
+D2H, H2D, D2D = 2, 1, 3
+
+
+def d2h(ptr: int, nbytes: int, dtype=np.uint8) -> np.ndarray:
+    out = np.empty(nbytes, np.uint8)
+    if nbytes:
+        st = hip().hipMemcpy(out.ctypes.data_as(C.c_void_p), C.c_void_p(ptr), nbytes, D2H)
+        assert st == 0, st
+    return out.view(dtype)
+
+
+def to_device(a: np.ndarray):
+    import torch
+
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def empty_device(n: int, dtype):
+    import torch
+
+    return torch.empty(n, dtype=dtype, device="cuda")
+
+
+def sync():
+    import torch
+
+    torch.cuda.synchronize()
+
+
+def parse_archive(arch: bytes, bklen=1024):
+    """Split a cuSZ archive into its segments (header.h:19-48, hf.h:40-46)."""
+    import struct
+
+    import cusz_amd
+
+    h = cusz_amd.psz_header.from_buffer_copy(arch[:176])
+    phf = arch[h.entry[2]:h.entry[3]]
+    bklen_, sublen, pardeg = struct.unpack_from("<iii", phf, 0)
+    bklen_ &= 0xFFFF
+    orig, tnbit, tncell = struct.unpack_from("<QQQ", phf, 16)
+    pent = struct.unpack_from("<6I", phf, 40)
+    rvbk = np.frombuffer(phf[pent[1]:pent[2]], np.uint8)
+    par_nbit = np.frombuffer(phf[pent[2]:pent[3]], np.uint32)
+    par_entry = np.frombuffer(phf[pent[3]:pent[4]], np.uint32)
+    bitstream = np.frombuffer(phf[pent[4]:pent[5]], np.uint32)
+    cells = np.frombuffer(arch[h.entry[3]:h.entry[4]], np.uint32).reshape(-1, 2)
+    return dict(header=h, phf=phf, bklen=bklen_, sublen=sublen, pardeg=pardeg, original_len=orig,
+                total_nbit=tnbit, total_ncell=tncell, phf_entry=pent, revbook=rvbk, par_nbit=par_nbit,
+                par_entry=par_entry, bitstream=bitstream, ol_val=cells[:, 0].view(np.float32).copy(),
+                ol_idx=cells[:, 1].copy())

@@ -1,0 +1,207 @@
+"""Parity of the HIP product path (through the C-ABI) against the CPU oracle.
+
+Bit-exact: quant codes, outlier set (index + value), histogram, codebook, the whole
+Huffman (phf) segment of the archive at the same chunk length, and the decompressed
+field (the oracle follows the reference's floating-point operation order).  Outlier
+cell ORDER is not compared (the reference's order is nondeterministic; ours is
+deterministic brick order) -- cells are compared sorted by index.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import cusz_amd as cz
+from cusz_amd import datagen
+from gpu_util import d2h, empty_device, parse_archive, sync, to_device
+
+pytestmark = pytest.mark.gpu
+
+
+def _field(kind, dims, dtype, seed):
+    n = int(np.prod(dims))
+    rng = np.random.default_rng(seed)
+    if kind == "smooth":
+        return datagen.smooth3d_np(dims, seed, dtype=dtype)
+    if kind == "walk":
+        return datagen.hacc1d_np(n, seed, jump=0.05, dtype=dtype)
+    if kind == "int":
+        return np.cumsum(rng.integers(-3, 4, n)).astype(dtype)
+    if kind == "noise":
+        return rng.standard_normal(n).astype(dtype)
+    raise ValueError(kind)
+
+
+def run_roundtrip(oracle, data, dims, eb, dtype=np.float32, zigzag=False, radius=512, sublen=0,
+                  check_bound=True):
+    n = int(np.prod(dims))
+    tdt = "float32" if dtype == np.float32 else "float64"
+    import torch
+
+    r = cz.Resource(cz.F4 if dtype == np.float32 else cz.F8, dims,
+                    cz.LorenzoZigZag if zigzag else cz.Lorenzo)
+    if sublen:
+        r.set_sublen(sublen)
+    d_in = to_device(data)
+    ptr, nbytes, st = r.compress(d_in.data_ptr(), eb, cz.Abs, radius)
+    arch = d2h(ptr, nbytes).tobytes()
+    a = parse_archive(arch)
+    h = a["header"]
+    assert h.entry[5] == nbytes == len(arch)
+    assert (h.len.x, h.len.y, h.len.z) == tuple(dims)
+
+    # ---- stage 1: quant codes and outliers vs oracle --------------------------------------
+    ino = r.internals()
+    codes_g = d2h(ino.d_quant_codes, 2 * n, np.uint16)
+    codes_o, ov_o, oi_o = oracle.lorenzo_c(data, dims, eb, radius, zigzag)
+    mism = np.flatnonzero(codes_g != codes_o)
+    assert mism.size == 0, f"{mism.size} code mismatches, first at {mism[:5]}"
+    order = np.argsort(a["ol_idx"], kind="stable")
+    np.testing.assert_array_equal(a["ol_idx"][order], oi_o)
+    np.testing.assert_array_equal(a["ol_val"][order].view(np.uint32), ov_o.view(np.uint32))
+    assert h.splen == len(oi_o)
+
+    # ---- stage 2: histogram, codebook, Huffman segment ------------------------------------
+    bklen = 2 * radius
+    hist_g = d2h(ino.d_hist, 4 * bklen, np.uint32)
+    np.testing.assert_array_equal(hist_g, oracle.histogram(codes_o, bklen))
+    seg_o, info = oracle.phf_segment(codes_o, bklen, sublen=a["sublen"])
+    np.testing.assert_array_equal(a["revbook"], info["revbook"])
+    np.testing.assert_array_equal(a["par_nbit"], info["par_nbit"])
+    np.testing.assert_array_equal(a["par_entry"], info["par_entry"])
+    np.testing.assert_array_equal(a["bitstream"], info["bitstream"])
+    assert a["phf"] == seg_o, "phf segment bytes differ"
+
+    # ---- stage 3: decompress into an un-zeroed, NaN-poisoned buffer -----------------------
+    out = empty_device(n, getattr(torch, tdt))
+    out.fill_(float("nan"))
+    r.decompress(ptr, nbytes, out.data_ptr())
+    sync()
+    xg = out.cpu().numpy()
+    xo = oracle.lorenzo_x(codes_o, ov_o, oi_o, dims, eb, radius, zigzag, dtype)
+    bad = np.flatnonzero(xg.view(np.uint64 if dtype == np.float64 else np.uint32) != xo.view(np.uint64 if dtype == np.float64 else np.uint32))
+    assert bad.size == 0, f"{bad.size} reconstruction mismatches, first {bad[:5]}: {xg[bad[:5]]} vs {xo[bad[:5]]}"
+    if check_bound:  # f32/f64 prequant rounding adds a few ulp of |x| (same in the reference)
+        tol = 1.001 * eb + 4 * float(np.spacing(np.abs(data).max().astype(dtype)))
+        assert np.max(np.abs(xg.astype(np.float64) - data)) <= tol
+    r.close()
+    return arch, a
+
+
+CASES = [
+    # (kind, dims, dtype, eb, zigzag, radius)
+    ("smooth", (1000, 1, 1), np.float32, 1e-3, False, 512),
+    ("smooth", (16384 * 3 + 11, 1, 1), np.float32, 1e-4, False, 512),
+    ("walk", (200_003, 1, 1), np.float32, 1e-4, False, 512),
+    ("smooth", (70, 45, 1), np.float32, 1e-3, False, 512),
+    ("smooth", (3600, 1800, 1), np.float32, 1e-4, False, 512),
+    ("smooth", (33, 17, 9), np.float32, 1e-3, False, 512),
+    ("smooth", (64, 64, 64), np.float32, 1e-4, False, 512),
+    ("smooth", (255, 257, 9), np.float32, 1e-4, False, 512),
+    ("smooth", (100, 60, 40), np.float32, 1e-4, False, 512),
+    ("smooth", (512, 256, 24), np.float32, 1e-4, False, 512),
+    ("smooth", (130, 70, 30), np.float64, 1e-5, False, 512),
+    ("smooth", (1000, 1, 1), np.float64, 1e-5, False, 512),
+    ("smooth", (301, 77, 1), np.float64, 1e-5, False, 512),
+    ("smooth", (64, 48, 40), np.float64, 1e-5, True, 512),
+    ("smooth", (64, 64, 64), np.float32, 1e-4, True, 512),
+    ("smooth", (5000, 1, 1), np.float32, 1e-4, True, 512),
+    ("smooth", (300, 100, 1), np.float32, 1e-4, True, 512),
+    ("smooth", (64, 40, 24), np.float32, 1e-3, False, 256),
+    ("smooth", (64, 40, 24), np.float32, 1e-3, False, 64),
+    ("int", (48, 40, 16), np.float32, 0.5, False, 512),
+    ("noise", (40, 40, 40), np.float32, 1e-2, False, 512),
+]
+
+
+@pytest.mark.parametrize("kind,dims,dtype,eb,zigzag,radius", CASES,
+                         ids=[f"{c[0]}-{'x'.join(map(str, c[1]))}-{np.dtype(c[2]).name}-{c[3]}-zz{int(c[4])}-r{c[5]}"
+                              for c in CASES])
+def test_parity_vs_oracle(oracle, kind, dims, dtype, eb, zigzag, radius):
+    data = _field(kind, dims, dtype, seed=sum(dims))
+    run_roundtrip(oracle, data, dims, eb, dtype, zigzag, radius)
+
+
+@pytest.mark.parametrize("sublen", [256, 1024, 4096])
+def test_parity_sublen_override(oracle, sublen):
+    dims = (64, 64, 32)
+    data = datagen.smooth3d_np(dims, 5)
+    arch, a = run_roundtrip(oracle, data, dims, 1e-4, sublen=sublen)
+    assert a["sublen"] == sublen
+
+
+@pytest.mark.parametrize("t,dims", [("t1", (256, 1, 1)), ("t2", (16, 16, 1)), ("t3", (8, 8, 8))])
+def test_reference_kat_on_gpu(oracle, t, dims):
+    """The reference's own KATs (correctness.inl) through the GPU path (eb=0.5)."""
+    from conftest import GOLDEN
+
+    k = np.load(os.path.join(GOLDEN, "kat_lorenzo.npz"))
+    arch, a = run_roundtrip(oracle, k[f"{t}_in"], dims, 0.5)
+    r = cz.Resource(cz.F4, dims)
+    d_in = to_device(k[f"{t}_in"])
+    r.compress(d_in.data_ptr(), 0.5)
+    codes = d2h(r.internals().d_quant_codes, 2 * int(np.prod(dims)), np.uint16)
+    np.testing.assert_array_equal(codes.astype(np.float32), k[f"{t}_comp_out"] + 512)
+
+
+def test_single_symbol_and_constant_field(oracle):
+    dims = (4096, 1, 1)
+    data = np.full(4096, 0.0, np.float32)
+    arch, a = run_roundtrip(oracle, data, dims, 1e-3)
+    assert a["total_nbit"] == 4096  # 1-bit code per symbol (DESIGN.md deviation)
+
+
+def test_decompress_with_fresh_manager_from_header(oracle):
+    import torch
+
+    dims = (96, 80, 40)
+    data = datagen.smooth3d_np(dims, 9)
+    r = cz.Resource(cz.F4, dims)
+    d_in = to_device(data)
+    ptr, nbytes, _ = r.compress(d_in.data_ptr(), 1e-4)
+    arch = torch.from_numpy(d2h(ptr, nbytes).copy()).cuda()
+    h = cz.psz_header.from_buffer_copy(arch[:176].cpu().numpy().tobytes())
+    r2 = cz.Resource(None, None, header=h)
+    out = empty_device(data.size, torch.float32)
+    r2.decompress(arch.data_ptr(), nbytes, out.data_ptr())
+    sync()
+    assert np.max(np.abs(out.cpu().numpy().astype(np.float64) - data)) <= 1.001e-4
+
+
+def test_manager_reuse_resets_state(oracle):
+    """Appendix B.3: reusing a manager must not mix stale outliers/histogram."""
+    dims = (64, 64, 16)
+    r = cz.Resource(cz.F4, dims)
+    d1 = to_device(datagen.smooth3d_np(dims, 1))
+    d2 = to_device(datagen.smooth3d_np(dims, 2, noise=1e-2))
+    r.compress(d1.data_ptr(), 1e-4)
+    p2, n2, _ = r.compress(d2.data_ptr(), 1e-4)
+    a2 = parse_archive(d2h(p2, n2).tobytes())
+    codes, ov, oi = oracle.lorenzo_c(d2.cpu().numpy(), dims, 1e-4)
+    assert a2["header"].splen == len(oi)
+    np.testing.assert_array_equal(np.sort(a2["ol_idx"]), oi)
+
+
+def test_outlier_overflow_reports_warning():
+    """Beyond the reference's 10 % outlier capacity the call reports PSZ_WARN_OUTLIER_TOO_MANY."""
+    dims = (200_000, 1, 1)
+    data = np.random.default_rng(0).uniform(-1e3, 1e3, dims[0]).astype(np.float32)
+    r = cz.Resource(cz.F4, dims)
+    d_in = to_device(data)
+    with pytest.raises(cz.PszError) as e:
+        r.compress(d_in.data_ptr(), 1e-4)
+    assert e.value.status == cz.PSZ_WARN_OUTLIER_TOO_MANY
+
+
+def test_rel_mode(oracle):
+    dims = (80, 60, 20)
+    data = datagen.smooth3d_np(dims, 4) * 3.0 + 10.0
+    r = cz.Resource(cz.F4, dims)
+    d_in = to_device(data)
+    ptr, nbytes, _ = r.compress(d_in.data_ptr(), 1e-4, cz.Rel)
+    h = r.header
+    rng = float(data.max()) - float(data.min())
+    assert h.min_val == float(data.min()) and h.max_val == float(data.max())
+    assert h.rc.eb == 1e-4 * rng and h.user_input_eb == 1e-4
+    codes_o, _, _ = oracle.lorenzo_c(data, dims, 1e-4 * rng)
+    np.testing.assert_array_equal(d2h(r.internals().d_quant_codes, 2 * data.size, np.uint16), codes_o)
