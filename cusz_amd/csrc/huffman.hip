@@ -12,9 +12,11 @@
 //    ({flag, value} packed in one 8-byte agent-scope atomic, so the value IS the flag) and
 //    writes the cells straight into the archive, coalesced.  Codes are read once from HBM.
 //  * decode: one lane per chunk (reference semantics, hf_kernels.cuhip.inl:331-396) but
-//    table-driven: a 2^K-entry LDS lookup table resolves codes of <= K bits per step
-//    instead of one bit per step; longer codes fall back to the canonical first[]/entry[]
-//    search.  Four symbols are buffered per 8-byte store.
+//    table-driven: a 4096-entry LDS table resolves up to TWO codewords per lookup from the
+//    next 12 bits (the reference walks one bit per step); longer codes fall back to the
+//    canonical first[]/entry[] search.  The bitstream is fetched in 4-cell groups with the
+//    next group in flight, and symbols are staged per lane in LDS and written 32 B at a time
+//    (full write granules instead of 2-8 B partial writes).
 #include "common.hh"
 #include "kernels.hh"
 
@@ -73,28 +75,37 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wave
   return off + inc - v;
 }
 
-// read this thread's PER codes of a chunk (PER = sublen / 256) and apply f(word)
-template <typename F>
-__device__ __forceinline__ void for_my_codes(const uint16_t* __restrict__ codes, size_t start, int per,
-                                             int cnt, const uint32_t* s_book, F&& f)
+constexpr int kMaxPer = 32;  // sublen <= 8192
+
+// Pack this thread's codewords (MSB-first, starting at bit `pos` of the chunk) into the LDS
+// cell buffer.  Words that only this thread touches are plain stores; the first word (when
+// `pos` is not word aligned) and the trailing partial word may be shared with neighbouring
+// threads and are merged with LDS atomic OR (the buffer is zeroed beforehand).
+__device__ __forceinline__ void pack_words(uint32_t* cells, uint32_t pos, const uint32_t (&w)[kMaxPer], int mine)
 {
-  const int mine = threadIdx.x * per;
-  const uint16_t* p = codes + start + mine;
-  if ((per & 7) == 0 && mine + per <= cnt) {
-    for (int i = 0; i < per; i += 8) {
-      uint4 w = *reinterpret_cast<const uint4*>(p + i);
-      const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+  uint32_t q = pos >> 5;
+  uint64_t acc = 0;
+  uint32_t fill = pos & 31;  // bits already owned by earlier threads in word q
+  bool first = fill != 0;
 #pragma unroll
-      for (int h = 0; h < 4; h++) {
-        f(s_book[ws[h] & 0xFFFFu]);
-        f(s_book[ws[h] >> 16]);
-      }
+  for (int i = 0; i < kMaxPer; i++) {
+    if (i >= mine) break;
+    const uint32_t l = w[i] >> 27, v = w[i] & 0x07FFFFFFu;
+    acc |= (uint64_t)v << (64 - fill - l);
+    fill += l;
+    if (fill >= 32) {
+      const uint32_t word = (uint32_t)(acc >> 32);
+      if (first)
+        atomicOr(&cells[q], word);
+      else
+        cells[q] = word;
+      first = false;
+      acc <<= 32;
+      fill -= 32;
+      q++;
     }
   }
-  else {
-    for (int i = 0; i < per; i++)
-      if (mine + i < cnt) f(s_book[p[i]]);
-  }
+  if (fill) atomicOr(&cells[q], (uint32_t)(acc >> 32));
 }
 
 __global__ void __launch_bounds__(kEncThreads) k_hf_encode(HfEncodeArgs a, int G, int cellcap)
@@ -122,24 +133,33 @@ __global__ void __launch_bounds__(kEncThreads) k_hf_encode(HfEncodeArgs a, int G
     }
     const size_t start = (size_t)c * a.sublen;
     const int cnt = (int)((a.n - start) < (size_t)a.sublen ? (a.n - start) : (size_t)a.sublen);
+    // this thread's codes [tid*per, tid*per + per) -> codewords in registers
+    const int lo = threadIdx.x * per;
+    const int mine = cnt - lo < 0 ? 0 : (cnt - lo < per ? cnt - lo : per);
+    const uint16_t* p = a.codes + start + lo;
+    uint32_t w[kMaxPer];
     uint32_t bits = 0;
-    for_my_codes(a.codes, start, per, cnt, s_book, [&](uint32_t w) { bits += w >> 27; });
-    uint32_t total;
-    uint32_t pos = block_excl_scan(bits, s_wave, total);
-    uint32_t* cells = s_cells + j * cellcap;
-    // MSB-first pack (hf_kernels.cuhip.inl:114-151) into LDS cells
-    for_my_codes(a.codes, start, per, cnt, s_book, [&](uint32_t w) {
-      const uint32_t l = w >> 27, v = w & 0x07FFFFFFu;
-      const uint32_t q = pos >> 5, o = pos & 31;
-      if (o + l <= 32)
-        atomicOr(&cells[q], v << (32 - o - l));
-      else {
-        const uint32_t sp = o + l - 32;
-        atomicOr(&cells[q], v >> sp);
-        atomicOr(&cells[q + 1], v << (32 - sp));
+    if ((per & 7) == 0 && mine == per) {
+#pragma unroll
+      for (int i = 0; i < kMaxPer; i += 8) {
+        if (i >= per) break;
+        const uint4 v = *reinterpret_cast<const uint4*>(p + i);
+        const uint32_t vs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int h = 0; h < 4; h++) w[i + 2 * h] = s_book[vs[h] & 0xFFFFu], w[i + 2 * h + 1] = s_book[vs[h] >> 16];
       }
-      pos += l;
-    });
+    }
+    else {
+#pragma unroll
+      for (int i = 0; i < kMaxPer; i++)
+        if (i < mine) w[i] = s_book[p[i]];
+    }
+#pragma unroll
+    for (int i = 0; i < kMaxPer; i++)
+      if (i < mine) bits += w[i] >> 27;
+    uint32_t total;
+    const uint32_t pos = block_excl_scan(bits, s_wave, total);
+    if (mine) pack_words(s_cells + j * cellcap, pos, w, mine);
     if (threadIdx.x == 0) s_nbit[j] = total;
   }
   __syncthreads();
@@ -194,30 +214,65 @@ __global__ void __launch_bounds__(kEncThreads) k_hf_encode(HfEncodeArgs a, int G
   }
 }
 
-constexpr int kLutBits = 10;
+constexpr int kLutBits = 12;           // 4096-entry LDS table
+constexpr int kDecThreads = 256;
+constexpr int kRing = 32;               // per-lane output ring (symbols)
+constexpr int kRingStride = 36;         // u32 words per lane (16-B aligned, spreads banks)
 
-__global__ void __launch_bounds__(256) k_hf_decode(HfDecodeArgs a)
+// LUT entry: [31:30] nsym (0 = long code), [29:25] consumed bits, [24:15] sym1, [14:5] sym0.
+__device__ __forceinline__ uint32_t lut_pack(uint32_t nsym, uint32_t bits, uint32_t s0, uint32_t s1)
+{
+  return (nsym << 30) | (bits << 25) | (s1 << 15) | (s0 << 5);
+}
+
+// canonical decode of one symbol from the top `have` bits of v (reference rule,
+// hf_kernels.cuhip.inl:351-365: the first l with prefix_l >= first[l]); returns length or 0
+__device__ __forceinline__ uint32_t canon_one(uint32_t v, int have, const uint32_t* first, const uint32_t* entry,
+                                              const uint16_t* keys, int bklen, int maxl, uint32_t& sym)
+{
+  for (int l = 1; l <= have && l <= maxl; l++) {
+    const uint32_t p = v >> (have - l);
+    if (p >= first[l]) {
+      uint32_t k = entry[l] + p - first[l];
+      sym = keys[k < (uint32_t)bklen ? k : (uint32_t)bklen - 1];
+      return (uint32_t)l;
+    }
+  }
+  return 0;
+}
+
+__global__ void __launch_bounds__(kDecThreads) k_hf_decode(HfDecodeArgs a)
 {
   __shared__ uint32_t lut[1 << kLutBits];
   __shared__ uint32_t s_first[32], s_entry[32];
   __shared__ uint16_t s_keys[kMaxBklen];
+  __shared__ __attribute__((aligned(16))) uint32_t ring[kDecThreads * kRingStride];
+  __shared__ int s_maxl;
 
   const int32_t* rv = reinterpret_cast<const int32_t*>(a.revbook);
   if (threadIdx.x < 32) s_first[threadIdx.x] = (uint32_t)rv[threadIdx.x], s_entry[threadIdx.x] = (uint32_t)rv[32 + threadIdx.x];
   const uint16_t* keys = reinterpret_cast<const uint16_t*>(a.revbook + 256);
   for (int i = threadIdx.x; i < a.bklen; i += blockDim.x) s_keys[i] = keys[i];
   __syncthreads();
-  // LUT: same rule as the reference decoder (first l with prefix >= first[l])
+  if (threadIdx.x == 0) {  // longest length: last l with a code (entry[l+1] > entry[l])
+    int m = 1;
+    for (int l = 1; l < 31; l++)
+      if (s_entry[l + 1] > s_entry[l]) m = l;
+    s_maxl = m;
+  }
+  __syncthreads();
+  const int maxl = s_maxl;
+  // two-symbol table (same rule as the reference decoder, applied twice)
   for (int i = threadIdx.x; i < (1 << kLutBits); i += blockDim.x) {
+    uint32_t s0 = 0, s1 = 0;
+    const uint32_t l0 = canon_one((uint32_t)i, kLutBits, s_first, s_entry, s_keys, a.bklen, maxl, s0);
     uint32_t e = 0;
-    for (int l = 1; l <= kLutBits; l++) {
-      const uint32_t v = (uint32_t)i >> (kLutBits - l);
-      if (v >= s_first[l]) {
-        uint32_t k = s_entry[l] + v - s_first[l];
-        if (k >= (uint32_t)a.bklen) k = a.bklen - 1;
-        e = ((uint32_t)s_keys[k] << 16) | (uint32_t)l;
-        break;
-      }
+    if (l0) {
+      const int rest = kLutBits - (int)l0;
+      const uint32_t l1 = rest > 0 ? canon_one((uint32_t)i & ((1u << rest) - 1), rest, s_first, s_entry, s_keys,
+                                               a.bklen, maxl, s1)
+                                   : 0u;
+      e = l1 ? lut_pack(2, l0 + l1, s0, s1) : lut_pack(1, l0, s0, 0);
     }
     lut[i] = e;
   }
@@ -225,47 +280,72 @@ __global__ void __launch_bounds__(256) k_hf_decode(HfDecodeArgs a)
 
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= a.pardeg) return;
-  const uint32_t* src = a.bitstream + a.par_entry[c];
-  const uint32_t nbit = a.par_nbit[c];
-  const uint32_t ncell = (nbit + 31) >> 5;
   const size_t obase = (size_t)c * a.sublen;
   if (obase >= a.n) return;
   const uint32_t nsym = (uint32_t)((a.n - obase) < (size_t)a.sublen ? (a.n - obase) : (size_t)a.sublen);
+  const uint32_t* src = a.bitstream + a.par_entry[c];
+  const uint32_t ncell = (a.par_nbit[c] + 31) >> 5;
   uint16_t* dst = a.out + obase;
+  uint16_t* my_ring = reinterpret_cast<uint16_t*>(ring + threadIdx.x * kRingStride);
 
-  auto cell = [&](uint32_t i) -> uint64_t { return i < ncell ? (uint64_t)src[i] : 0ull; };
-  uint64_t buf = (cell(0) << 32) | cell(1);
-  int avail = 64;
-  uint32_t ci = 2;
-  uint64_t pack = 0;
+  // bit supply: 4-cell groups, the next group's loads in flight while this one is consumed
+  auto ld = [&](uint32_t i) -> uint32_t { return i < ncell ? src[i] : 0u; };
+  uint32_t g0 = ld(0), g1 = ld(1), g2 = ld(2), g3 = ld(3);
+  uint32_t h0 = ld(4), h1 = ld(5), h2 = ld(6), h3 = ld(7);
+  uint32_t next = 8;
+  uint64_t buf = 0;
+  int avail = 0;
   uint32_t j = 0;
-  for (; j < nsym; j++) {
-    if (avail <= 32) {
-      buf |= cell(ci++) << (32 - avail);
-      avail += 32;
+
+  auto emit = [&](uint32_t sym) {
+    my_ring[j & (kRing - 1)] = (uint16_t)sym;
+    j++;
+    if ((j & 15) == 0) {  // a half ring is complete: 32 B to HBM
+      const uint4* q = reinterpret_cast<const uint4*>(my_ring + ((j - 16) & (kRing - 1)));
+      uint4* d = reinterpret_cast<uint4*>(dst + j - 16);
+      d[0] = q[0];
+      d[1] = q[1];
     }
-    const uint32_t e = lut[buf >> (64 - kLutBits)];
-    uint32_t l = e & 0xFFu, sym = e >> 16;
-    if (l == 0) {  // long code: canonical search (hf_kernels.cuhip.inl:351-365)
-      for (l = kLutBits + 1; l <= (uint32_t)kLmax; l++) {
-        const uint32_t v = (uint32_t)(buf >> (64 - l));
-        if (v >= s_first[l]) {
-          uint32_t k = s_entry[l] + v - s_first[l];
-          if (k >= (uint32_t)a.bklen) k = a.bklen - 1;
-          sym = s_keys[k];
-          break;
-        }
+  };
+
+  auto decode_some = [&]() {
+    while (avail > 32 && j < nsym) {
+      const uint32_t e = lut[buf >> (64 - kLutBits)];
+      const uint32_t ns = e >> 30;
+      if (ns) {
+        const uint32_t bits = (e >> 25) & 31u;
+        emit((e >> 5) & 1023u);
+        if (ns == 2 && j < nsym) emit((e >> 15) & 1023u);  // (a 2nd symbol past the chunk end is dropped)
+        buf <<= bits;
+        avail -= (int)bits;
+      }
+      else {  // code longer than the table: canonical search on up to 27 bits
+        uint32_t sym = 0;
+        const uint32_t l = canon_one((uint32_t)(buf >> (64 - kLmax)), kLmax, s_first, s_entry, s_keys, a.bklen,
+                                     maxl, sym);
+        const uint32_t ll = l ? l : 1u;
+        emit(sym);
+        buf <<= ll;
+        avail -= (int)ll;
       }
     }
-    buf <<= l;
-    avail -= (int)l;
-    pack |= (uint64_t)sym << (16 * (j & 3));
-    if ((j & 3) == 3) {
-      *reinterpret_cast<uint2*>(dst + j - 3) = make_uint2((uint32_t)pack, (uint32_t)(pack >> 32));
-      pack = 0;
-    }
+  };
+
+  while (j < nsym) {
+    buf |= (uint64_t)g0 << (32 - avail), avail += 32;
+    decode_some();
+    buf |= (uint64_t)g1 << (32 - avail), avail += 32;
+    decode_some();
+    buf |= (uint64_t)g2 << (32 - avail), avail += 32;
+    decode_some();
+    buf |= (uint64_t)g3 << (32 - avail), avail += 32;
+    decode_some();
+    g0 = h0, g1 = h1, g2 = h2, g3 = h3;
+    h0 = ld(next), h1 = ld(next + 1), h2 = ld(next + 2), h3 = ld(next + 3);
+    next += 4;
   }
-  for (uint32_t t = j & ~3u; t < j; t++) dst[t] = (uint16_t)(pack >> (16 * (t & 3)));
+  // tail: symbols not yet flushed
+  for (uint32_t t = j & ~15u; t < j; t++) dst[t] = my_ring[t & (kRing - 1)];
 }
 
 }  // namespace

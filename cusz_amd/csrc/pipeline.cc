@@ -221,7 +221,7 @@ struct Pipeline {
 
     // per-call state reset (the reference never resets these: SURVEY.md Appendix B.3)
     CUSZ_AMD_HIP_CHECK(hipMemsetAsync(d_hist, 0, (size_t)bklen * 4, stream));
-    CUSZ_AMD_HIP_CHECK(hipMemsetAsync(d_small, 0, 64, stream));
+    CUSZ_AMD_HIP_CHECK(hipMemsetAsync(d_small, 0, 64 + sizeof(CompressInfo), stream));
     CUSZ_AMD_HIP_CHECK(hipMemsetAsync(d_status, 0, status_words * 8, stream));
     mark(1);
 

@@ -19,27 +19,38 @@ __device__ __forceinline__ unsigned long long wsum64(unsigned long long v)
   return v;
 }
 
-// one workgroup of 1024 threads
+// sum of per-chunk bit counts: many blocks, one 64-bit atomic each (total_nbit zeroed before)
+__global__ void __launch_bounds__(256) k_sum_nbit(const uint32_t* __restrict__ par_nbit, int pardeg,
+                                                  unsigned long long* total)
+{
+  __shared__ unsigned long long s_red[4];
+  unsigned long long acc = 0;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < pardeg; i += gridDim.x * 256) acc += par_nbit[i];
+  acc = wsum64(acc);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(total, s_red[0] + s_red[1] + s_red[2] + s_red[3]);
+}
+
+// one workgroup of 1024 threads: exclusive scan of per-brick outlier counts (8 per thread
+// per pass) and the archive totals
 __global__ void __launch_bounds__(1024) k_finalize_scan(FinalizeArgs a)
 {
-  __shared__ unsigned long long s_red[16];
   __shared__ uint32_t s_scan[16];
   __shared__ uint32_t s_carry;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-
-  // total bits = sum(par_nbit)
-  unsigned long long acc = 0;
-  for (int i = tid; i < a.pardeg; i += 1024) acc += a.par_nbit[i];
-  acc = wsum64(acc);
-  if (lane == 0) s_red[wid] = acc;
   if (tid == 0) s_carry = 0;
   __syncthreads();
-
-  // exclusive scan of per-brick outlier counts (clamped to the slot capacity)
-  for (uint32_t base = 0; base < a.nbricks; base += 1024) {
-    const uint32_t b = base + tid;
-    const uint32_t v = b < a.nbricks ? min(a.brick_cnt[b], a.cap_per_brick) : 0u;
-    uint32_t inc = v;
+  constexpr int PER = 8;
+  for (uint32_t base = 0; base < a.nbricks; base += 1024 * PER) {
+    uint32_t v[PER], sum = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const uint32_t b = base + tid * PER + k;
+      v[k] = b < a.nbricks ? min(a.brick_cnt[b], a.cap_per_brick) : 0u;
+      sum += v[k];
+    }
+    uint32_t inc = sum;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       uint32_t t = __shfl_up(inc, d);
@@ -49,27 +60,29 @@ __global__ void __launch_bounds__(1024) k_finalize_scan(FinalizeArgs a)
     __syncthreads();
     uint32_t off = s_carry;
     for (int w = 0; w < wid; w++) off += s_scan[w];
-    if (b < a.nbricks) a.brick_off[b] = off + inc - v;
+    uint32_t run = off + inc - sum;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const uint32_t b = base + tid * PER + k;
+      if (b < a.nbricks) a.brick_off[b] = run;
+      run += v[k];
+    }
     __syncthreads();
     if (tid == 1023) s_carry = off + inc;
     __syncthreads();
   }
 
   if (tid == 0) {
-    unsigned long long tb = 0;
-    for (int w = 0; w < 16; w++) tb += s_red[w];
     const int last = a.pardeg - 1;
     const unsigned long long ncell =
         last >= 0 ? (unsigned long long)a.par_entry[last] + ((a.par_nbit[last] + 31u) >> 5) : 0ull;
     const uint32_t slot_total = s_carry;
     const uint32_t sp = *a.spill_cnt;
     const uint32_t sp_kept = sp < a.spill_cap ? sp : a.spill_cap;
-    unsigned long long clamped = 0;  // cells beyond a full slot always went to the spill list
     a.brick_off[a.nbricks] = slot_total;
-    a.info->total_nbit = tb;
     a.info->total_ncell = ncell;
     a.info->splen = (unsigned long long)slot_total + sp_kept;
-    a.info->outlier_lost = (sp > a.spill_cap ? sp - a.spill_cap : 0u) + clamped;
+    a.info->outlier_lost = sp > a.spill_cap ? sp - a.spill_cap : 0u;
   }
 }
 
@@ -171,6 +184,9 @@ __global__ void k_extrema_final(const double* part, int nparts, double* out)
 
 int launch_finalize_scan(const FinalizeArgs& a, hipStream_t st)
 {
+  int grid = (a.pardeg + 255) / 256;
+  grid = grid < 1 ? 1 : (grid > 128 ? 128 : grid);
+  k_sum_nbit<<<grid, 256, 0, st>>>(a.par_nbit, a.pardeg, &a.info->total_nbit);
   k_finalize_scan<<<1, 1024, 0, st>>>(a);
   return (int)hipGetLastError();
 }
