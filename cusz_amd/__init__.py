@@ -14,7 +14,7 @@ import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "lib", "libcusz_amd.so")
+LIB_PATH = os.environ.get("CUSZ_AMD_LIB") or os.path.join(HERE, "lib", "libcusz_amd.so")
 CLI_PATH = os.path.join(HERE, "bin", "cusz")
 
 # ---- enums (include/c_type.h, include/cusz/type.h) --------------------------------------

@@ -94,6 +94,16 @@ int launch_write_headers(uint8_t* archive, const void* psz_hdr_tpl, const void* 
                          const CompressInfo* info, size_t phf_offset, size_t bitstream_rel,
                          hipStream_t st);
 
+// small host<->device transfers through host-mapped pinned memory (no stream sync)
+struct XferRegions {
+  int count;
+  int nwords[4];
+  uint32_t* dst[4];
+  const uint32_t* src[4];
+};
+int launch_publish(const XferRegions& r, uint32_t* flag, uint32_t epoch, hipStream_t st);
+int launch_upload(const XferRegions& r, hipStream_t st);
+
 // min / max (Rel mode, extrema.cuhip.inl:86-208), writes {min, max} as doubles
 template <typename T>
 int launch_extrema(const T* in, size_t n, double* d_minmax, unsigned int* d_scratch, hipStream_t st);

@@ -46,6 +46,32 @@ __device__ __forceinline__ int16_t zz_dec(uint16_t u)
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// value of lane (l - L) when both lanes lie in the same TILE_LANES-aligned group.  Groups of
+// <= 16 lanes never cross a DPP row, so a row_shr:L DPP move does it in one VALU op (no LDS
+// permute); wider groups fall back to ds_bpermute (__shfl_up).
+template <int L>
+__device__ __forceinline__ int dpp_shr(int v)
+{
+  static_assert(L >= 1 && L <= 15, "row_shr range");
+  return __builtin_amdgcn_update_dpp(0, v, 0x110 + L, 0xf, 0xf, false);
+}
+
+template <typename T, int L, int TILE_LANES>
+__device__ __forceinline__ T shr_in_tile(T v)
+{
+  if constexpr (TILE_LANES <= 16) {
+    if constexpr (sizeof(T) == 4)
+      return __builtin_bit_cast(T, dpp_shr<L>(__builtin_bit_cast(int, v)));
+    else {
+      const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+      const int lo = dpp_shr<L>((int)(uint32_t)u), hi = dpp_shr<L>((int)(uint32_t)(u >> 32));
+      return __builtin_bit_cast(T, (unsigned long long)(uint32_t)lo | ((unsigned long long)(uint32_t)hi << 32));
+    }
+  }
+  else
+    return __shfl_up(v, L);
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
 // ---- vector row I/O -------------------------------------------------------------------
@@ -266,16 +292,20 @@ __device__ __forceinline__ void hs_step(T (&t)[V], uint32_t x0)
   for (int k = 0; k < V; k++) old[k] = t[k];
 #pragma unroll
   for (int k = 0; k < V; k++) {
-    constexpr int dummy = 0;
-    (void)dummy;
     const int kk = k - D;
     T src;
     if (kk >= 0)
       src = old[kk >= 0 ? kk : 0];
     else {
+      constexpr int TL = TW / V;  // lanes per tile
       const int L = (-kk + V - 1) / V;
       const int k2 = kk + L * V;
-      src = __shfl_up(old[k2], L);
+      if (L == 1) src = shr_in_tile<T, 1, TL>(old[k2]);
+      else if (L == 2) src = shr_in_tile<T, 2, TL>(old[k2]);
+      else if (L == 3) src = shr_in_tile<T, 3, TL>(old[k2]);
+      else if (L == 4) src = shr_in_tile<T, 4, TL>(old[k2]);
+      else if (L == 8) src = shr_in_tile<T, 8, TL>(old[k2]);
+      else src = __shfl_up(old[k2], L);
     }
     const uint32_t px = (x0 + k) % TW;
     if (px >= (uint32_t)D) t[k] = old[k] + src;
@@ -358,7 +388,7 @@ k_lorenzo_c2d(const T* __restrict__ in, uint32_t lx, uint32_t ly, T ebx2_r, T r,
       T a[V];
 #pragma unroll
       for (int k = 0; k < V; k++) a[k] = p[k] - pprev[k], pprev[k] = p[k];
-      const T west = __shfl_up(a[V - 1], 1);
+      const T west = shr_in_tile<T, 1, 32 / V>(a[V - 1]);
       T d[V];
 #pragma unroll
       for (int k = V - 1; k > 0; k--) d[k] = a[k] - a[k - 1];
@@ -406,7 +436,7 @@ k_lorenzo_c3d(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
       // x-difference inside 8-wide tiles
 #pragma unroll
       for (int z = 0; z < 8; z++) {
-        const T west = __shfl_up(p[z][V - 1], 1);
+        const T west = shr_in_tile<T, 1, 8 / V>(p[z][V - 1]);
 #pragma unroll
         for (int k = V - 1; k > 0; k--) p[z][k] = p[z][k] - p[z][k - 1];
         if (x0 % 8 != 0) p[z][0] = p[z][0] - west;

@@ -20,6 +20,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <tuple>
 
 #include "common.hh"
 #include "cusz.h"
@@ -89,11 +90,15 @@ struct Pipeline {
   uint8_t* d_archive = nullptr;
   size_t archive_cap = 0;
 
-  // pinned host
-  uint32_t* h_hist = nullptr;
-  uint32_t* h_book = nullptr;
-  uint8_t* h_revbook = nullptr;
-  uint8_t* h_readback = nullptr;  // psz_header | CompressInfo | minmax
+  // pinned, host-mapped, coherent transfer area (kernels write it, the host polls flags)
+  uint8_t* h_xfer = nullptr;
+  uint32_t epoch = 0;
+  static constexpr size_t kXferBytes = 16384;
+  volatile uint32_t* flag(int i) { return reinterpret_cast<volatile uint32_t*>(h_xfer) + i; }  // 0..15
+  uint32_t* h_hist() { return reinterpret_cast<uint32_t*>(h_xfer + 64); }               // 4 KB
+  uint32_t* h_book() { return reinterpret_cast<uint32_t*>(h_xfer + 64 + 4096); }        // 4 KB
+  uint8_t* h_revbook() { return h_xfer + 64 + 8192; }                                    // 2304 B
+  uint8_t* h_readback() { return h_xfer + 64 + 8192 + 2560; }                            // 1 KB
 
   bool timing = false;
   hipEvent_t ev[12] = {};
@@ -113,13 +118,12 @@ struct Pipeline {
     for (void* p : {(void*)d_codes, (void*)d_hist, (void*)d_book, (void*)d_slots, (void*)d_brick_cnt,
                     (void*)d_brick_off, (void*)d_spill, (void*)d_small, (void*)d_status, (void*)d_archive})
       if (p) (void)hipFree(p);
-    for (void* p : {(void*)h_hist, (void*)h_book, (void*)h_revbook, (void*)h_readback})
-      if (p) (void)hipHostFree(p);
+    if (h_xfer) (void)hipHostFree(h_xfer);
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e), e = nullptr;
     d_codes = nullptr, d_hist = nullptr, d_book = nullptr, d_slots = nullptr, d_brick_cnt = nullptr;
     d_brick_off = nullptr, d_spill = nullptr, d_small = nullptr, d_status = nullptr, d_archive = nullptr;
-    h_hist = nullptr, h_book = nullptr, h_revbook = nullptr, h_readback = nullptr;
+    h_xfer = nullptr;
   }
 
   size_t rvbk_bytes(int bklen) const { return 4 * 64 + 2 * (size_t)bklen; }
@@ -154,10 +158,8 @@ struct Pipeline {
     CUSZ_AMD_HIP_CHECK(hipMalloc(&d_small, kSmallBytes));
     CUSZ_AMD_HIP_CHECK(hipMemset(d_small, 0, kSmallBytes));
     CUSZ_AMD_HIP_CHECK(alloc_chunk_state());
-    CUSZ_AMD_HIP_CHECK(hipHostMalloc(&h_hist, kMaxBklen * 4, hipHostMallocDefault));
-    CUSZ_AMD_HIP_CHECK(hipHostMalloc(&h_book, kMaxBklen * 4, hipHostMallocDefault));
-    CUSZ_AMD_HIP_CHECK(hipHostMalloc(&h_revbook, 4 * 64 + 2 * kMaxBklen, hipHostMallocDefault));
-    CUSZ_AMD_HIP_CHECK(hipHostMalloc(&h_readback, 1024, hipHostMallocDefault));
+    CUSZ_AMD_HIP_CHECK(hipHostMalloc(&h_xfer, kXferBytes, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(h_xfer, 0, kXferBytes);
     for (auto& e : ev) CUSZ_AMD_HIP_CHECK(hipEventCreate(&e));
     return PSZ_SUCCESS;
   }
@@ -172,6 +174,32 @@ struct Pipeline {
     archive_cap = 176 + 128 + rvbk_bytes(kMaxBklen) + 8 * (size_t)pardeg + 4 * bitstream_cells_cap() +
                   8 * ((size_t)geom.nbricks * cap_per_brick + spill_cap) + 64;
     return hipMalloc(&d_archive, archive_cap);
+  }
+
+  // device words -> host-mapped memory, then wait for the flag (fallback: stream sync)
+  int fetch(XferRegions r, int fl)
+  {
+    const uint32_t e = ++epoch;
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_publish(r, const_cast<uint32_t*>(flag(fl)), e, stream));
+    for (long spin = 0;; spin++) {
+      if (__atomic_load_n(flag(fl), __ATOMIC_ACQUIRE) == e) return PSZ_SUCCESS;
+      if (spin > (1L << 26)) break;  // ~seconds: something is wrong, surface it via the runtime
+      __builtin_ia32_pause();
+    }
+    CUSZ_AMD_HIP_CHECK(hipStreamSynchronize(stream));
+    return __atomic_load_n(flag(fl), __ATOMIC_ACQUIRE) == e ? PSZ_SUCCESS : PSZ_ABORT_NOT_IMPLEMENTED;
+  }
+
+  static XferRegions regions(std::initializer_list<std::tuple<void*, const void*, size_t>> l)
+  {
+    XferRegions r{};
+    for (auto& [d, s, bytes] : l) {
+      r.dst[r.count] = (uint32_t*)d;
+      r.src[r.count] = (const uint32_t*)s;
+      r.nwords[r.count] = (int)((bytes + 3) / 4);
+      r.count++;
+    }
+    return r;
   }
 
   void mark(int i)
@@ -210,10 +238,10 @@ struct Pipeline {
     // Rel mode: eb *= (max - min)  (libcusz.cc:287-293; range in double of T extrema)
     if (h->rc.mode == Rel) {
       CUSZ_AMD_HIP_CHECK((hipError_t)launch_extrema<T>(in, n, minmax(), ext_scratch(), stream));
-      CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(h_readback + 512, minmax(), 16, hipMemcpyDeviceToHost, stream));
-      CUSZ_AMD_HIP_CHECK(hipStreamSynchronize(stream));
+      int fs = fetch(regions({{h_readback() + 512, minmax(), 16}}), 1);
+      if (fs) return fs;
       double mm[2];
-      std::memcpy(mm, h_readback + 512, 16);
+      std::memcpy(mm, h_readback() + 512, 16);
       h->min_val = mm[0], h->max_val = mm[1];
       h->rc.eb *= (mm[1] - mm[0]);
     }
@@ -231,15 +259,15 @@ struct Pipeline {
     mark(2);
 
     // codebook on the host (hf_hl.cc:21-34), one round trip
-    CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(h_hist, d_hist, (size_t)bklen * 4, hipMemcpyDeviceToHost, stream));
-    CUSZ_AMD_HIP_CHECK(hipStreamSynchronize(stream));
-    const int rv = build_codebook(h_hist, bklen, h_book, h_revbook);
+    int fs = fetch(regions({{h_hist(), d_hist, (size_t)bklen * 4}}), 2);
+    if (fs) return fs;
+    const int rv = build_codebook(h_hist(), bklen, h_book(), h_revbook());
     const size_t phf_off = 176;  // + anchor bytes (0 for Lorenzo)
     const size_t rvbk = (size_t)rv;
     const size_t nbit_rel = 128 + rvbk, entry_rel = nbit_rel + 4 * (size_t)pardeg;
     const size_t bits_rel = entry_rel + 4 * (size_t)pardeg;
-    CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(d_book, h_book, (size_t)bklen * 4, hipMemcpyHostToDevice, stream));
-    CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(d_archive + phf_off + 128, h_revbook, rvbk, hipMemcpyHostToDevice, stream));
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_upload(
+        regions({{d_book, h_book(), (size_t)bklen * 4}, {d_archive + phf_off + 128, h_revbook(), rvbk}}), stream));
     mark(3);
 
     HfEncodeArgs ea{d_codes,
@@ -275,17 +303,19 @@ struct Pipeline {
     ph.entry[4] = (uint32_t)bits_rel;
     CUSZ_AMD_HIP_CHECK(
         (hipError_t)launch_write_headers(d_archive, h, &ph, info(), phf_off, bits_rel, stream));
-    CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(h_readback, d_archive, 176, hipMemcpyDeviceToHost, stream));
-    CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(h_readback + 256, info(), sizeof(CompressInfo), hipMemcpyDeviceToHost, stream));
-    CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(h_readback + 384, timeout(), 4, hipMemcpyDeviceToHost, stream));
     mark(5);
-    CUSZ_AMD_HIP_CHECK(hipStreamSynchronize(stream));
+    fs = fetch(regions({{h_readback(), d_archive, 176},
+                        {h_readback() + 256, info(), sizeof(CompressInfo)},
+                        {h_readback() + 384, timeout(), 4}}),
+               3);
+    if (fs) return fs;
+    if (timing) CUSZ_AMD_HIP_CHECK(hipEventSynchronize(ev[5]));
 
     CompressInfo ci;
-    std::memcpy(&ci, h_readback + 256, sizeof(ci));
+    std::memcpy(&ci, h_readback() + 256, sizeof(ci));
     unsigned int tmo;
-    std::memcpy(&tmo, h_readback + 384, 4);
-    std::memcpy(h, h_readback, 176);
+    std::memcpy(&tmo, h_readback() + 384, 4);
+    std::memcpy(h, h_readback(), 176);
     splen = (size_t)ci.splen;
     if (timing) {
       stage_ms[PSZ_AMD_T_EXTREMA] = span(0, 1);
@@ -479,7 +509,7 @@ int psz_compress_analyize_float(psz_resource* m, psz_rc2 rc, float* in, u4* expo
   int s = compress_impl<float>(m, rc, in, nullptr, &dummy, &bytes);
   if (s != PSZ_SUCCESS && s != PSZ_WARN_RADIUS_TOO_LARGE) return s;
   Pipeline* p = cusz_amd::P(m);
-  std::memcpy(exported_h_hist, p->h_hist, sizeof(u4) * 2 * m->header->rc.radius);
+  std::memcpy(exported_h_hist, p->h_hist(), sizeof(u4) * 2 * m->header->rc.radius);
   return s;
 }
 

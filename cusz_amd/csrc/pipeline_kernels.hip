@@ -180,7 +180,37 @@ __global__ void k_extrema_final(const double* part, int nparts, double* out)
   out[0] = mn, out[1] = mx;
 }
 
+// Copy device words into host-mapped (coherent, pinned) memory, then raise a flag the host
+// polls.  Replaces hipMemcpyAsync(D2H) + hipStreamSynchronize on the compress critical path.
+__global__ void __launch_bounds__(256) k_publish(XferRegions r, uint32_t* flag, uint32_t epoch)
+{
+  for (int k = 0; k < r.count; k++)
+    for (int i = threadIdx.x; i < r.nwords[k]; i += 256) r.dst[k][i] = r.src[k][i];
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Copy host-mapped words (written by the host before this launch) into device memory.
+__global__ void __launch_bounds__(256) k_upload(XferRegions r)
+{
+  for (int k = 0; k < r.count; k++)
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < r.nwords[k]; i += gridDim.x * 256) r.dst[k][i] = r.src[k][i];
+}
+
 }  // namespace
+
+int launch_publish(const XferRegions& r, uint32_t* flag, uint32_t epoch, hipStream_t st)
+{
+  k_publish<<<1, 256, 0, st>>>(r, flag, epoch);
+  return (int)hipGetLastError();
+}
+
+int launch_upload(const XferRegions& r, hipStream_t st)
+{
+  k_upload<<<4, 256, 0, st>>>(r);
+  return (int)hipGetLastError();
+}
 
 int launch_finalize_scan(const FinalizeArgs& a, hipStream_t st)
 {
