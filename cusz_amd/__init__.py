@@ -97,7 +97,7 @@ EXPORTS = [
     "phf_version", "phf_versioninfo",
     # cusz_amd.h
     "psz_amd_get_internals", "psz_amd_enable_timing", "psz_amd_stage_times", "psz_amd_set_sublen",
-    "psz_amd_decode_codes", "psz_amd_version",
+    "psz_amd_decode_codes", "psz_amd_set_decoder", "psz_amd_version",
 ]
 
 
@@ -137,12 +137,17 @@ def lib():
     L.psz_amd_stage_times.argtypes = [P, C.POINTER(C.c_float), C.c_int]
     L.psz_amd_set_sublen.argtypes = [P, C.c_int]
     L.psz_amd_decode_codes.argtypes = [P, P]
+    L.psz_amd_set_decoder.argtypes = [P, C.c_int]
     L.psz_amd_version.restype = C.c_char_p
     L.phf_coarse_tune.argtypes = [C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.pszheader_filesize.restype = C.c_size_t
     L.pszheader_filesize.argtypes = [C.POINTER(psz_header)]
     _lib = L
     return L
+
+
+# Huffman decoder selection (include/cusz_amd.h PSZ_AMD_DECODER_*)
+DECODER_AUTO, DECODER_LANE, DECODER_WAVE = 0, 1, 2
 
 
 class PszError(RuntimeError):
@@ -216,6 +221,12 @@ class Resource:
 
     def set_sublen(self, s: int):
         lib().psz_amd_set_sublen(self._h, s)
+
+    def set_decoder(self, kind: int):
+        """0 auto, 1 one lane per chunk, 2 one wave per chunk (PSZ_AMD_DECODER_*)."""
+        st = lib().psz_amd_set_decoder(self._h, int(kind))
+        if st != PSZ_SUCCESS:
+            raise PszError(st, "psz_amd_set_decoder")
 
     def decode_codes(self, d_archive: int):
         st = lib().psz_amd_decode_codes(self._h, C.c_void_p(d_archive))

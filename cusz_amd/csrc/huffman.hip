@@ -11,12 +11,11 @@
 //    the group's global cell offset by decoupled look-back over per-group status words
 //    ({flag, value} packed in one 8-byte agent-scope atomic, so the value IS the flag) and
 //    writes the cells straight into the archive, coalesced.  Codes are read once from HBM.
-//  * decode: one lane per chunk (reference semantics, hf_kernels.cuhip.inl:331-396) but
-//    table-driven: a 4096-entry LDS table resolves up to TWO codewords per lookup from the
-//    next 12 bits (the reference walks one bit per step); longer codes fall back to the
-//    canonical first[]/entry[] search.  The bitstream is fetched in 4-cell groups with the
-//    next group in flight, and symbols are staged per lane in LDS and written 32 B at a time
-//    (full write granules instead of 2-8 B partial writes).
+//  * decode: the reference decodes one chunk per thread, bit by bit (hf_kernels.cuhip.inl:
+//    331-396) -- 65,536 serial threads at 512^3.  Here one WAVE decodes a chunk: its bits are
+//    split into 64 segments decoded in parallel from guessed starts, corrected by Huffman
+//    self-synchronisation; a 4096-entry LDS table resolves up to two codewords per lookup;
+//    cells and output are staged in LDS so HBM sees coalesced reads and 16-B writes.
 #include "common.hh"
 #include "kernels.hh"
 
@@ -81,14 +80,15 @@ constexpr int kMaxPer = 32;  // sublen <= 8192
 // cell buffer.  Words that only this thread touches are plain stores; the first word (when
 // `pos` is not word aligned) and the trailing partial word may be shared with neighbouring
 // threads and are merged with LDS atomic OR (the buffer is zeroed beforehand).
-__device__ __forceinline__ void pack_words(uint32_t* cells, uint32_t pos, const uint32_t (&w)[kMaxPer], int mine)
+template <int N>
+__device__ __forceinline__ void pack_words(uint32_t* cells, uint32_t pos, const uint32_t (&w)[N], int mine)
 {
   uint32_t q = pos >> 5;
   uint64_t acc = 0;
   uint32_t fill = pos & 31;  // bits already owned by earlier threads in word q
   bool first = fill != 0;
 #pragma unroll
-  for (int i = 0; i < kMaxPer; i++) {
+  for (int i = 0; i < N; i++) {
     if (i >= mine) break;
     const uint32_t l = w[i] >> 27, v = w[i] & 0x07FFFFFFu;
     acc |= (uint64_t)v << (64 - fill - l);
@@ -214,138 +214,655 @@ __global__ void __launch_bounds__(kEncThreads) k_hf_encode(HfEncodeArgs a, int G
   }
 }
 
-constexpr int kLutBits = 12;           // 4096-entry LDS table
-constexpr int kDecThreads = 256;
-constexpr int kRing = 32;               // per-lane output ring (symbols)
-constexpr int kRingStride = 36;         // u32 words per lane (16-B aligned, spreads banks)
+// ---- wave-per-chunk encoder ------------------------------------------------------------------
+// Same output as k_hf_encode; each wave owns one chunk, so the bit offsets come from a wave
+// scan (no workgroup barrier per chunk) and the four chunks of a workgroup are packed
+// concurrently.  Codes are read 16 per lane per round (two 16-B loads, issued for the next
+// round before the current one is packed).  The workgroup's cell offset comes from the same
+// decoupled look-back.
+constexpr int kEncW = 4;    // chunks (waves) per workgroup
+constexpr int kRound = 16;  // codes per lane per round
 
-// LUT entry: [31:30] nsym (0 = long code), [29:25] consumed bits, [24:15] sym1, [14:5] sym0.
-__device__ __forceinline__ uint32_t lut_pack(uint32_t nsym, uint32_t bits, uint32_t s0, uint32_t s1)
+__device__ __forceinline__ void load_codes16(const uint16_t* p, int mine, uint32_t (&v)[8], bool vec)
 {
-  return (nsym << 30) | (bits << 25) | (s1 << 15) | (s0 << 5);
-}
-
-// canonical decode of one symbol from the top `have` bits of v (reference rule,
-// hf_kernels.cuhip.inl:351-365: the first l with prefix_l >= first[l]); returns length or 0
-__device__ __forceinline__ uint32_t canon_one(uint32_t v, int have, const uint32_t* first, const uint32_t* entry,
-                                              const uint16_t* keys, int bklen, int maxl, uint32_t& sym)
-{
-  for (int l = 1; l <= have && l <= maxl; l++) {
-    const uint32_t p = v >> (have - l);
-    if (p >= first[l]) {
-      uint32_t k = entry[l] + p - first[l];
-      sym = keys[k < (uint32_t)bklen ? k : (uint32_t)bklen - 1];
-      return (uint32_t)l;
+  if (vec) {
+    const uint4 a = reinterpret_cast<const uint4*>(p)[0], b = reinterpret_cast<const uint4*>(p)[1];
+    v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w, v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
+  }
+  else {
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint32_t lo = 2 * i < mine ? p[2 * i] : 0u, hi = 2 * i + 1 < mine ? p[2 * i + 1] : 0u;
+      v[i] = lo | (hi << 16);
     }
   }
-  return 0;
 }
 
-__global__ void __launch_bounds__(kDecThreads) k_hf_decode(HfDecodeArgs a)
+__global__ void __launch_bounds__(64 * kEncW) k_hf_encode_w(HfEncodeArgs a, int cellcap)
 {
-  __shared__ uint32_t lut[1 << kLutBits];
-  __shared__ uint32_t s_first[32], s_entry[32];
-  __shared__ uint16_t s_keys[kMaxBklen];
-  __shared__ __attribute__((aligned(16))) uint32_t ring[kDecThreads * kRingStride];
-  __shared__ int s_maxl;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint32_t* s_book = smem;                                  // bklen words (rounded to 4)
+  uint32_t* s_cells = smem + ((a.bklen + 3) & ~3);          // kEncW * cellcap words
+  __shared__ uint32_t s_nbit[kEncW];
+  __shared__ uint32_t s_base;
 
-  const int32_t* rv = reinterpret_cast<const int32_t*>(a.revbook);
-  if (threadIdx.x < 32) s_first[threadIdx.x] = (uint32_t)rv[threadIdx.x], s_entry[threadIdx.x] = (uint32_t)rv[32 + threadIdx.x];
+  for (int i = threadIdx.x; i < a.bklen; i += blockDim.x) s_book[i] = a.book[i];
+  for (int i = threadIdx.x; i < kEncW * cellcap / 4; i += blockDim.x)
+    reinterpret_cast<uint4*>(s_cells)[i] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+
+  const int g = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = g * kEncW + wid;
+  uint32_t nbits = 0;
+  if (c < a.pardeg) {
+    const size_t start = (size_t)c * a.sublen;
+    const int cnt = (int)((a.n - start) < (size_t)a.sublen ? (a.n - start) : (size_t)a.sublen);
+    const int per = a.sublen / 64 < kRound ? a.sublen / 64 : kRound;  // codes per lane per round
+    const int span = per * 64;
+    uint32_t* cells = s_cells + wid * cellcap;
+    const uint16_t* src = a.codes + start;
+    const bool vec_ok = per == kRound;
+    uint32_t nxt[8];
+    {
+      const int lo = lane * per, mine = min(max(cnt - lo, 0), per);
+      load_codes16(src + lo, mine, nxt, vec_ok && mine == per);
+    }
+    for (int r0 = 0; r0 < cnt; r0 += span) {
+      const int lo = r0 + lane * per, mine = min(max(cnt - lo, 0), per);
+      uint32_t cur[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) cur[i] = nxt[i];
+      if (r0 + span < cnt) {  // prefetch the next round
+        const int lo2 = lo + span, mine2 = min(max(cnt - lo2, 0), per);
+        load_codes16(src + lo2, mine2, nxt, vec_ok && mine2 == per);
+      }
+      uint32_t w[kRound], bits = 0;
+#pragma unroll
+      for (int i = 0; i < kRound; i++) {
+        const uint32_t code = (cur[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
+        w[i] = i < mine ? s_book[code] : 0u;
+        bits += w[i] >> 27;
+      }
+      const uint32_t inc = wave_incl_scan(bits, lane);
+      if (mine) pack_words<kRound>(cells, nbits + inc - bits, w, mine);
+      nbits += __shfl(inc, 63);
+    }
+  }
+  if (lane == 0) s_nbit[wid] = nbits;
+  __syncthreads();
+
+  uint32_t gcells = 0;
+  for (int j = 0; j < kEncW; j++) gcells += (s_nbit[j] + 31) >> 5;
+
+  // decoupled look-back over group status words
+  if (threadIdx.x < 64) {
+    uint32_t base = 0;
+    if (g == 0) {
+      if (lane == 0) st_status(&a.status[0], kFlagIncl | gcells);
+    }
+    else {
+      if (lane == 0) st_status(&a.status[g], kFlagAgg | gcells);
+      int j = g - 1;
+      unsigned int spins = 0;
+      while (true) {
+        const int idx = j - lane;
+        const unsigned long long st = idx >= 0 ? ld_status(&a.status[idx]) : kFlagIncl;
+        const uint32_t flag = (uint32_t)(st >> 32);
+        if (__ballot(flag == 0)) {
+          if (++spins > kSpinLimit) {
+            if (lane == 0) atomicOr(a.timeout, 1u);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        const unsigned long long incl = __ballot(flag == 2);
+        const int first = incl ? (__ffsll((long long)incl) - 1) : 64;
+        base += wave_sum(lane <= first ? (uint32_t)st : 0u);
+        if (incl) break;
+        j -= 64;
+      }
+      if (lane == 0) st_status(&a.status[g], kFlagIncl | (unsigned long long)(base + gcells));
+    }
+    if (lane == 0) s_base = base;
+  }
+  __syncthreads();
+
+  // each wave writes its own chunk (cells start on a fresh cell per chunk)
+  uint32_t off = s_base;
+  for (int j = 0; j < wid; j++) off += (s_nbit[j] + 31) >> 5;
+  if (c < a.pardeg) {
+    const uint32_t nb = s_nbit[wid], nc = (nb + 31) >> 5;
+    if (lane == 0) a.par_nbit[c] = nb, a.par_entry[c] = off;
+    const uint32_t* cells = s_cells + wid * cellcap;
+    for (uint32_t i = lane; i < nc; i += 64) a.bitstream[off + i] = cells[i];
+  }
+}
+
+// ============================== decode ======================================================
+// Tables (built once per decompress by k_hf_tables into a device scratch, copied to LDS):
+//  L1: 4096 entries indexed by the next 12 stream bits.  A normal entry resolves one or two
+//      whole codewords: [31:30] nsym (1|2), [29:25] bits of the nsym codes, [24:20] length of
+//      the first code, [19:10] second symbol, [9:0] first symbol.  A prefix that only starts
+//      codes longer than 12 bits holds a pointer: nsym = 0, [29:25] k, [15:0] offset of a
+//      2^k-entry L2 subtable indexed by the k bits after the prefix.
+//  L2: single-symbol entries of the long codes; slot 0 is 0 ("not tabulated").
+// Canonical codes put every long code below first[12] (hf_canon.seq.cc construction: longer
+// codes are numerically smaller), so the pointer prefixes are exactly [0, first[12]) and the
+// longest code under a prefix is the one holding its smallest window value.
+constexpr int kLutBits = 12;
+constexpr int kL1 = 1 << kLutBits;
+constexpr int kTabMaxl = kL1;       // longest code length
+constexpr int kTabFirst = kL1 + 1;  // [32] first[l] (0 beyond the longest code)
+constexpr int kTabBase = kL1 + 33;  // [32] entry[l] - first[l]
+constexpr int kTabL2 = kL1 + 128;   // second level
+constexpr int kL2Cap = 2048;        // power of two
+static_assert(kTabL2 + kL2Cap <= kHfDecTableWords, "decode table scratch too small");
+constexpr int kLongLens = kLmax - kLutBits;  // lengths only the slow path resolves
+
+__device__ __forceinline__ uint32_t lut_pack(uint32_t nsym, uint32_t bits, uint32_t l0, uint32_t s0, uint32_t s1)
+{
+  return (nsym << 30) | (bits << 25) | (l0 << 20) | (s1 << 10) | s0;
+}
+
+__device__ __forceinline__ int longest_code(const uint32_t* entry)
+{
+  int m = 1;  // last l with a code (entry[l+1] > entry[l])
+  for (int l = 1; l < 31; l++)
+    if (entry[l + 1] > entry[l]) m = l;
+  return m;
+}
+
+// One symbol from a left-justified window, reference rule (hf_kernels.cuhip.inl:351-365: the
+// first length l with prefix_l >= first[l]).  The thresholds first[l] * 2^(32-l) never increase
+// with l (canonical construction: first[l] >= (first[l+1] + count[l+1]) / 2), so the lengths
+// that fail form a prefix 1..m and the code length is 1 + the number of failing lengths.
+// (The prefix form prefix_l < first[l] is exact even when first[l] = 2^l.)
+__device__ __forceinline__ uint32_t tab_decode1(uint32_t v, const uint32_t (&first)[kLmax + 1], int maxl,
+                                                const uint32_t* base, const uint16_t* keys, uint32_t bklen,
+                                                uint32_t& sym)
+{
+  uint32_t l = 1;
+#pragma unroll
+  for (int k = 1; k <= kLmax; k++) l += (k <= maxl && (v >> (32 - k)) < first[k]) ? 1u : 0u;
+  if (l > (uint32_t)maxl) l = (uint32_t)maxl;
+  sym = keys[min(base[l] + (v >> (32 - l)), bklen - 1)];
+  return l;
+}
+
+__global__ void __launch_bounds__(1024) k_hf_tables(const uint8_t* revbook, int bklen, uint32_t* tab)
+{
+  __shared__ uint32_t s_first[32], s_entry[32], s_base[32];
+  __shared__ uint16_t s_keys[kMaxBklen];
+  __shared__ uint16_t s_off[kL1];
+  __shared__ uint8_t s_k[kL1];
+  __shared__ uint32_t s_wave[16];
+  const int tid = threadIdx.x;
+  const int32_t* rv = reinterpret_cast<const int32_t*>(revbook);
+  if (tid < 32) s_first[tid] = (uint32_t)rv[tid], s_entry[tid] = (uint32_t)rv[32 + tid];
+  const uint16_t* keys = reinterpret_cast<const uint16_t*>(revbook + 256);
+  for (int i = tid; i < bklen; i += blockDim.x) s_keys[i] = keys[i];
+  __syncthreads();
+  const int maxl = longest_code(s_entry);
+  if (tid < 32) {
+    // slow-path copy of first[l] (0xFFFFFFFF past the longest code: never below it)
+    tab[kTabFirst + tid] = (tid >= 1 && tid <= maxl) ? s_first[tid] : 0u;
+    s_base[tid] = s_entry[tid] - s_first[tid];
+    tab[kTabBase + tid] = s_entry[tid] - s_first[tid];
+  }
+  if (tid == 0) tab[kTabMaxl] = (uint32_t)maxl, tab[kTabL2] = 0u;
+  __syncthreads();
+  uint32_t thr[kLmax + 1];  // first[l]
+#pragma unroll
+  for (int k = 0; k <= kLmax; k++) thr[k] = s_first[k];
+  const uint32_t ub = (uint32_t)bklen;
+  const uint32_t P = maxl > kLutBits ? min(s_first[kLutBits], (uint32_t)kL1) : 0u;
+
+  // L1 entries (4 prefixes per thread) and the L2 subtable sizes of the pointer prefixes
+  uint32_t e[4], sz[4], tot = 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const uint32_t i = (uint32_t)tid * 4 + j, v = i << (32 - kLutBits);
+    uint32_t s0, s1;
+    const uint32_t l0 = tab_decode1(v, thr, maxl, s_base, s_keys, ub, s0);
+    e[j] = 0, sz[j] = 0;
+    if (i >= P && l0 <= (uint32_t)kLutBits) {
+      const uint32_t rest = kLutBits - l0;
+      const uint32_t l1 = rest ? tab_decode1(v << l0, thr, maxl, s_base, s_keys, ub, s1) : 99u;
+      e[j] = l1 <= rest ? lut_pack(2, l0 + l1, l0, s0, s1) : lut_pack(1, l0, l0, s0, 0);
+    }
+    else if (i < P && l0 > (uint32_t)kLutBits && l0 <= (uint32_t)kLmax) {
+      sz[j] = 1u << (l0 - kLutBits);  // <= 2^15
+    }
+    tot += sz[j];
+  }
+  // workgroup exclusive scan of the subtable sizes; offsets start at 1
+  const int lane = tid & 63, wid = tid >> 6;
+  uint32_t inc = tot;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t t = __shfl_up(inc, d);
+    if (lane >= d) inc += t;
+  }
+  if (lane == 63) s_wave[wid] = inc;
+  __syncthreads();
+  uint32_t off = 1;
+  for (int w = 0; w < wid; w++) off += s_wave[w];
+  off += inc - tot;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const uint32_t i = (uint32_t)tid * 4 + j;
+    if (sz[j]) {
+      const uint32_t k = 31 - __clz(sz[j]);
+      const bool fits = off + sz[j] <= (uint32_t)kL2Cap;
+      e[j] = fits ? ((k << 25) | off) : 0u;  // 0: slow path
+      s_k[i] = fits ? (uint8_t)k : 0;
+      s_off[i] = (uint16_t)(fits ? off : 0);
+      off += sz[j];
+    }
+    else if (i < P) {
+      s_k[i] = 0;  // (inconsistent book) slow path
+    }
+    tab[i] = e[j];
+  }
+  __syncthreads();
+  for (uint32_t p = 0; p < P; p++) {
+    const uint32_t k = s_k[p];
+    if (!k) continue;
+    const uint32_t o = s_off[p];
+    for (uint32_t j = tid; j < (1u << k); j += blockDim.x) {
+      const uint32_t v = (p << (32 - kLutBits)) | (j << (32 - kLutBits - k));
+      uint32_t s;
+      const uint32_t l = tab_decode1(v, thr, maxl, s_base, s_keys, ub, s);
+      tab[kTabL2 + o + j] = lut_pack(1, l, l, s, 0);
+    }
+  }
+}
+
+__device__ __forceinline__ void wave_sync()
+{
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+struct HfTables {
+  const uint32_t* l1;
+  const uint32_t* l2;
+  const uint32_t* base;  // entry[l] - first[l]
+  const uint16_t* keys;
+  uint32_t bklen;
+  uint32_t first[kLongLens];  // first[l], l = 13..27 (wave-uniform, SGPRs)
+};
+
+// entry for the codeword(s) at the top of `win`: L1, then L2 for long codes (branch-free --
+// with 64 lanes some lane almost always holds a long code), then the rare untabulated case.
+__device__ __forceinline__ uint32_t hf_entry(const HfTables& t, uint32_t win)
+{
+  const uint32_t e1 = t.l1[win >> (32 - kLutBits)];
+  const uint32_t k = (e1 >> 25) & 31u;
+  const uint32_t j = (win << kLutBits) >> 1 >> (31 - k);  // the k bits after the prefix (0 if k = 0)
+  const uint32_t e2 = t.l2[((e1 & 0xFFFFu) + j) & (uint32_t)(kL2Cap - 1)];
+  uint32_t e = (e1 >> 30) ? e1 : e2;
+  if (__builtin_expect(!(e >> 30), 0)) {  // not tabulated: count thresholds (lengths > 12)
+    uint32_t l = kLutBits + 1;
+#pragma unroll
+    for (int q = 0; q < kLongLens; q++) l += (win >> (32 - (kLutBits + 1 + q))) < t.first[q] ? 1u : 0u;
+    if (l > kLmax) l = kLmax;
+    const uint32_t s = t.keys[min(t.base[l] + (win >> (32 - l)), t.bklen - 1)];
+    e = lut_pack(1, l, l, s, 0);
+  }
+  return e;
+}
+
+template <typename Tab>
+__device__ __forceinline__ void load_tables(const HfDecodeArgs& a, uint32_t* s_l1, uint32_t* s_l2, uint32_t* s_base,
+                                            uint16_t* s_keys, Tab& tb)
+{
   const uint16_t* keys = reinterpret_cast<const uint16_t*>(a.revbook + 256);
   for (int i = threadIdx.x; i < a.bklen; i += blockDim.x) s_keys[i] = keys[i];
-  __syncthreads();
-  if (threadIdx.x == 0) {  // longest length: last l with a code (entry[l+1] > entry[l])
-    int m = 1;
-    for (int l = 1; l < 31; l++)
-      if (s_entry[l + 1] > s_entry[l]) m = l;
-    s_maxl = m;
-  }
-  __syncthreads();
-  const int maxl = s_maxl;
-  // two-symbol table (same rule as the reference decoder, applied twice)
-  for (int i = threadIdx.x; i < (1 << kLutBits); i += blockDim.x) {
-    uint32_t s0 = 0, s1 = 0;
-    const uint32_t l0 = canon_one((uint32_t)i, kLutBits, s_first, s_entry, s_keys, a.bklen, maxl, s0);
-    uint32_t e = 0;
-    if (l0) {
-      const int rest = kLutBits - (int)l0;
-      const uint32_t l1 = rest > 0 ? canon_one((uint32_t)i & ((1u << rest) - 1), rest, s_first, s_entry, s_keys,
-                                               a.bklen, maxl, s1)
-                                   : 0u;
-      e = l1 ? lut_pack(2, l0 + l1, s0, s1) : lut_pack(1, l0, s0, 0);
-    }
-    lut[i] = e;
-  }
-  __syncthreads();
+  for (int i = threadIdx.x; i < kL1 / 4; i += blockDim.x)
+    reinterpret_cast<uint4*>(s_l1)[i] = reinterpret_cast<const uint4*>(a.lut)[i];
+  for (int i = threadIdx.x; i < kL2Cap / 4; i += blockDim.x)
+    reinterpret_cast<uint4*>(s_l2)[i] = reinterpret_cast<const uint4*>(a.lut + kTabL2)[i];
+  if (threadIdx.x < 32) s_base[threadIdx.x] = a.lut[kTabBase + threadIdx.x];
+  tb.l1 = s_l1;
+  tb.l2 = s_l2;
+  tb.base = s_base;
+  tb.keys = s_keys;
+  tb.bklen = (uint32_t)a.bklen;
+#pragma unroll
+  for (int q = 0; q < kLongLens; q++) tb.first[q] = __builtin_amdgcn_readfirstlane(a.lut[kTabFirst + kLutBits + 1 + q]);
+}
 
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= a.pardeg) return;
+// ---- lane-per-chunk decoder (the reference's decomposition, hf_kernels.cuhip.inl:331-396) ----
+// Each lane decodes one whole chunk, so there is no synchronisation pass and every codeword is
+// decoded once.  Per lane: a 4-block (16-cell) LDS ring fed by 16-B loads issued two cadences
+// ahead (two alternating register slots, so the wait for one never waits for the other), and
+// a 32-symbol LDS output ring flushed in 32-B stores.  Steps are taken in cadences of kCad
+// (uniform across the wave) so refills and flushes happen at wave-uniform points.
+constexpr int kLpcThreads = 256;
+constexpr int kInStride = 20;   // words per lane: 16 ring cells + 1 mirror + pad (16-B aligned)
+constexpr int kOutStride = 20;  // words per lane: 32 symbols + pad
+constexpr int kCad = 4;         // <= 4 * 27 bits consumed per cadence < one 128-bit block
+
+__global__ void __launch_bounds__(kLpcThreads) k_hf_decode_lane(HfDecodeArgs a)
+{
+  __shared__ __attribute__((aligned(16))) uint32_t s_l1[kL1];
+  __shared__ __attribute__((aligned(16))) uint32_t s_l2[kL2Cap];
+  __shared__ uint32_t s_base[32];
+  __shared__ uint16_t s_keys[kMaxBklen];
+  __shared__ __attribute__((aligned(16))) uint32_t s_in[kLpcThreads * kInStride];
+  __shared__ __attribute__((aligned(16))) uint32_t s_out[kLpcThreads * kOutStride];
+  HfTables tb;
+  load_tables(a, s_l1, s_l2, s_base, s_keys, tb);
+
+  const uint32_t c = blockIdx.x * kLpcThreads + threadIdx.x;
   const size_t obase = (size_t)c * a.sublen;
-  if (obase >= a.n) return;
-  const uint32_t nsym = (uint32_t)((a.n - obase) < (size_t)a.sublen ? (a.n - obase) : (size_t)a.sublen);
-  const uint32_t* src = a.bitstream + a.par_entry[c];
-  const uint32_t ncell = (a.par_nbit[c] + 31) >> 5;
-  uint16_t* dst = a.out + obase;
-  uint16_t* my_ring = reinterpret_cast<uint16_t*>(ring + threadIdx.x * kRingStride);
-
-  // bit supply: 4-cell groups, the next group's loads in flight while this one is consumed
-  auto ld = [&](uint32_t i) -> uint32_t { return i < ncell ? src[i] : 0u; };
-  uint32_t g0 = ld(0), g1 = ld(1), g2 = ld(2), g3 = ld(3);
-  uint32_t h0 = ld(4), h1 = ld(5), h2 = ld(6), h3 = ld(7);
-  uint32_t next = 8;
-  uint64_t buf = 0;
-  int avail = 0;
-  uint32_t j = 0;
-
-  auto emit = [&](uint32_t sym) {
-    my_ring[j & (kRing - 1)] = (uint16_t)sym;
-    j++;
-    if ((j & 15) == 0) {  // a half ring is complete: 32 B to HBM
-      const uint4* q = reinterpret_cast<const uint4*>(my_ring + ((j - 16) & (kRing - 1)));
-      uint4* d = reinterpret_cast<uint4*>(dst + j - 16);
-      d[0] = q[0];
-      d[1] = q[1];
+  const bool live = c < (uint32_t)a.pardeg && obase < a.n;
+  const uint32_t nsym = live ? (uint32_t)min((size_t)a.sublen, a.n - obase) : 0u;
+  const uint32_t nbit = live ? a.par_nbit[c] : 0u;
+  const uint32_t entry = live ? a.par_entry[c] : 0u;
+  const uint32_t ncell = (nbit + 31) >> 5;
+  // 16-B aligned view of this chunk's cells: block b = bytes [16b, 16b+16) from `gb`
+  const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(a.bitstream + entry) & 15);
+  const uint4* gb = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.bitstream + entry) - mis);
+  const uint32_t skip = mis >> 2;
+  const uint32_t nblk = (skip + ncell + 3) >> 2;
+  const bool tail = live && c + 1 == (uint32_t)a.pardeg;  // last chunk: never read past its cells
+  // every call issues exactly one 16-B load (so the compiler can wait for one pending slot
+  // without waiting for the other); the last chunk's final partial block is re-read by cells
+  const uint4* gsafe = reinterpret_cast<const uint4*>(a.lut);
+  auto load_block = [&](uint32_t b) -> uint4 {
+    const uint32_t bb = min(b, nblk ? nblk - 1 : 0u);
+    const bool partial = tail && (bb + 1) * 4 > skip + ncell;
+    uint4 v = *((live && !partial) ? gb + bb : gsafe);
+    if (partial) {
+      const uint32_t* q = reinterpret_cast<const uint32_t*>(gb + bb);
+      const uint32_t lim = skip + ncell - bb * 4;  // valid cells in this block (1..3)
+      v.x = q[0];
+      v.y = lim > 1 ? q[1] : 0u;
+      v.z = lim > 2 ? q[2] : 0u;
+      v.w = 0u;
     }
+    return v;
+  };
+  uint32_t* ring = s_in + threadIdx.x * kInStride;
+  uint16_t* oring = reinterpret_cast<uint16_t*>(s_out + threadIdx.x * kOutStride);
+  auto ring_put = [&](uint32_t b, const uint4& v) {
+    reinterpret_cast<uint4*>(ring)[b & 3] = v;
+    if ((b & 3) == 0) ring[16] = v.x;  // mirror: a window starting in cell 15 reads cell 0 as cell 16
   };
 
-  auto decode_some = [&]() {
-    while (avail > 32 && j < nsym) {
-      const uint32_t e = lut[buf >> (64 - kLutBits)];
-      const uint32_t ns = e >> 30;
-      if (ns) {
-        const uint32_t bits = (e >> 25) & 31u;
-        emit((e >> 5) & 1023u);
-        if (ns == 2 && j < nsym) emit((e >> 15) & 1023u);  // (a 2nd symbol past the chunk end is dropped)
-        buf <<= bits;
-        avail -= (int)bits;
-      }
-      else {  // code longer than the table: canonical search on up to 27 bits
-        uint32_t sym = 0;
-        const uint32_t l = canon_one((uint32_t)(buf >> (64 - kLmax)), kLmax, s_first, s_entry, s_keys, a.bklen,
-                                     maxl, sym);
-        const uint32_t ll = l ? l : 1u;
-        emit(sym);
-        buf <<= ll;
-        avail -= (int)ll;
-      }
-    }
-  };
-
-  while (j < nsym) {
-    buf |= (uint64_t)g0 << (32 - avail), avail += 32;
-    decode_some();
-    buf |= (uint64_t)g1 << (32 - avail), avail += 32;
-    decode_some();
-    buf |= (uint64_t)g2 << (32 - avail), avail += 32;
-    decode_some();
-    buf |= (uint64_t)g3 << (32 - avail), avail += 32;
-    decode_some();
-    g0 = h0, g1 = h1, g2 = h2, g3 = h3;
-    h0 = ld(next), h1 = ld(next + 1), h2 = ld(next + 2), h3 = ld(next + 3);
-    next += 4;
+  // prologue: up to 4 blocks into the ring, two more in flight
+  uint32_t ld = min(nblk, 4u);
+  {
+    uint4 v[4];
+#pragma unroll
+    for (int b = 0; b < 4; b++) v[b] = load_block(b);
+#pragma unroll
+    for (int b = 0; b < 4; b++)
+      if ((uint32_t)b < ld) ring_put(b, v[b]);
   }
-  // tail: symbols not yet flushed
-  for (uint32_t t = j & ~15u; t < j; t++) dst[t] = my_ring[t & (kRing - 1)];
+  uint32_t bA = ld, bB = ld + 1;
+  uint4 pA = load_block(bA), pB = load_block(bB);
+
+  uint32_t pos = skip * 32, cnt = 0, flushed = 0;
+  uint16_t* gout = a.out + obase;
+
+  auto steps = [&]() {
+#pragma unroll
+    for (int s = 0; s < kCad; s++) {
+      if (cnt < nsym) {
+        const uint32_t* rp = ring + ((pos >> 5) & 15u);
+        const uint32_t win = (uint32_t)((((uint64_t)rp[0] << 32) | rp[1]) >> (32 - (pos & 31u)));
+        const uint32_t e = hf_entry(tb, win);
+        const uint32_t l0 = (e >> 20) & 31u;
+        const bool both = (e >> 30) == 2u && cnt + 1 < nsym;
+        const uint32_t i0 = cnt & 31u, i1 = both ? ((cnt + 1) & 31u) : i0;
+        oring[i0] = (uint16_t)(e & 1023u);
+        oring[i1] = (uint16_t)(both ? ((e >> 10) & 1023u) : (e & 1023u));
+        cnt += both ? 2u : 1u;
+        pos += both ? ((e >> 25) & 31u) : l0;
+      }
+    }
+  };
+  auto cadence = [&](uint4& p, uint32_t& b) {
+    if (b == ld && ld < nblk && ld - (pos >> 7) < 4u) {
+      ring_put(ld, p);
+      ld++;
+    }
+    if (b < ld) b += 2;
+    p = load_block(b);
+    if (cnt - flushed >= 16u) {
+      const uint4* src = reinterpret_cast<const uint4*>(oring + (flushed & 16u));
+      uint4* dst = reinterpret_cast<uint4*>(gout + flushed);
+      const uint4 v0 = src[0], v1 = src[1];
+      dst[0] = v0;
+      dst[1] = v1;
+      flushed += 16;
+    }
+  };
+  while (__any(cnt < nsym)) {
+    steps();
+    cadence(pA, bA);
+    steps();
+    cadence(pB, bB);
+  }
+  wave_sync();
+  for (uint32_t i = flushed; i < cnt; i++) gout[i] = oring[i & 31u];
+}
+
+// ---- wave-per-chunk decoder (for few, long chunks) ------------------------------------------
+constexpr int kDecWaves = 4;   // waves per decode workgroup
+constexpr int kSyncWin = 64;   // bits of a segment whose codeword starts are remembered
+
+#ifdef CUSZ_AMD_DEC_PROFILE
+// per-wave phase clocks and step counts (diagnostic build only; read by psz_amd_debug_decode_profile)
+__device__ unsigned long long g_dec_prof[4096 * 16];
+#define DP_STEP(x) (x)++
+#else
+#define DP_STEP(x) (void)0
+#endif
+
+// the 32 stream bits starting at bit `pos` (MSB-first cells)
+template <bool GLOBAL>
+__device__ __forceinline__ uint32_t window(const uint32_t* cells, uint32_t ncell, uint32_t pos)
+{
+  const uint32_t w = pos >> 5;
+  const uint32_t c0 = cells[w];
+  const uint32_t c1 = GLOBAL ? (w + 1 < ncell ? cells[w + 1] : 0u) : cells[w + 1];
+  return (uint32_t)((((uint64_t)c0 << 32) | c1) >> (32 - (pos & 31)));
+}
+
+// One table step at `pos`: returns the bits consumed and the codewords counted (1 or 2; the
+// second only if it starts before `hi`).  `l0` = length of the first codeword, syms in s0/s1.
+template <bool GLOBAL>
+__device__ __forceinline__ uint32_t dec_step(const uint32_t* cells, uint32_t ncell, uint32_t pos, uint32_t hi,
+                                             const HfTables& t, uint32_t& n, uint32_t& l0, uint32_t& s0,
+                                             uint32_t& s1)
+{
+  const uint32_t e = hf_entry(t, window<GLOBAL>(cells, ncell, pos));
+  l0 = (e >> 20) & 31u;
+  s0 = e & 1023u;
+  s1 = (e >> 10) & 1023u;
+  const bool both = (e >> 30) == 2 && pos + l0 < hi;
+  n = both ? 2u : 1u;
+  return both ? ((e >> 25) & 31u) : l0;
+}
+
+// Pass A: count codewords starting in [lo, hi) from the guess lo; remember which of the first
+// kSyncWin bits are codeword starts on this path (bm).  Returns the count; end = first start >= hi.
+template <bool GLOBAL>
+__device__ __forceinline__ uint32_t pass_count(const uint32_t* cells, uint32_t ncell, uint32_t lo, uint32_t hi,
+                                               const HfTables& t, uint32_t& end, uint64_t& bm, uint32_t& steps)
+{
+  uint32_t cnt = 0, pos = lo;
+  bm = 0;
+  while (pos < hi) {
+    DP_STEP(steps);
+    uint32_t n, l0, s0, s1;
+    const uint32_t adv = dec_step<GLOBAL>(cells, ncell, pos, hi, t, n, l0, s0, s1);
+    const uint32_t d = pos - lo;
+    if (d < kSyncWin) {
+      bm |= 1ull << d;
+      if (n == 2 && d + l0 < kSyncWin) bm |= 1ull << (d + l0);
+    }
+    cnt += n;
+    pos += adv;
+  }
+  end = pos;
+  return cnt;
+}
+
+// Re-count from the corrected start s (>= lo).  Huffman codes self-synchronise: once this path
+// lands on a codeword start of pass A's path (bm), the rest of the segment is pass A's.
+template <bool GLOBAL>
+__device__ __forceinline__ uint32_t pass_resync(const uint32_t* cells, uint32_t ncell, uint32_t lo, uint32_t hi,
+                                                uint32_t s, const HfTables& t, uint64_t bm, uint32_t cnt_a,
+                                                uint32_t end_a, uint32_t& end, uint32_t& steps)
+{
+  uint32_t cnt = 0, pos = s;
+  while (pos < hi) {
+    DP_STEP(steps);
+    const uint32_t d = pos - lo;
+    if (d < kSyncWin && ((bm >> d) & 1ull)) {
+      end = end_a;
+      return cnt + cnt_a - (uint32_t)__builtin_popcountll(bm & ((1ull << d) - 1ull));
+    }
+    uint32_t n, l0, s0, s1;
+    pos += dec_step<GLOBAL>(cells, ncell, pos, hi, t, n, l0, s0, s1);
+    cnt += n;
+  }
+  end = pos;
+  return cnt;
+}
+
+template <bool GLOBAL>
+__device__ __forceinline__ void pass_emit(const uint32_t* cells, uint32_t ncell, uint32_t pos, uint32_t hi,
+                                          const HfTables& t, uint16_t* out, uint32_t& steps)
+{
+  while (pos < hi) {
+    DP_STEP(steps);
+    uint32_t n, l0, s0, s1;
+    pos += dec_step<GLOBAL>(cells, ncell, pos, hi, t, n, l0, s0, s1);
+    out[0] = (uint16_t)s0;
+    if (n == 2) out[1] = (uint16_t)s1;
+    out += n;
+  }
+}
+
+struct DecProf {
+#ifdef CUSZ_AMD_DEC_PROFILE
+  unsigned long long v[16] = {0};
+  unsigned long long t = 0;
+  __device__ void start() { t = __builtin_readcyclecounter(); }
+  __device__ void mark(int k)
+  {
+    const unsigned long long n = __builtin_readcyclecounter();
+    v[k] += n - t;
+    t = n;
+  }
+  __device__ void add(int k, uint32_t x) { v[k] += x; }
+  __device__ void add_max(int k, uint32_t x)
+  {
+    for (int d = 32; d > 0; d >>= 1) x = max(x, (uint32_t)__shfl_xor(x, d));
+    v[k] += x;
+  }
+#else
+  __device__ void start() {}
+  __device__ void mark(int) {}
+  __device__ void add(int, uint32_t) {}
+  __device__ void add_max(int, uint32_t) {}
+#endif
+};
+
+template <bool GLOBAL>
+__device__ __forceinline__ void decode_chunk(const uint32_t* cells, uint32_t ncell, uint32_t nbit, uint32_t nsym,
+                                             const HfTables& t, uint16_t* outs, int lane, DecProf& pf)
+{
+  const uint32_t seg = (nbit + 63) / 64;
+  const uint32_t lo = min(lane * seg, nbit), hi = min(lo + seg, nbit);
+  uint32_t end_a, st_a = 0, st_r = 0, st_e = 0;
+  uint64_t bm;
+  const uint32_t cnt_a = pass_count<GLOBAL>(cells, ncell, lo, hi, t, end_a, bm, st_a);
+  pf.mark(1);
+  uint32_t start = lo, cnt = cnt_a, end = end_a;
+  int it = 0;
+  for (; it < 64; it++) {
+    uint32_t s_new = __shfl_up(end, 1);
+    if (lane == 0) s_new = 0;
+    const bool changed = s_new != start;
+    if (!__ballot(changed)) break;
+    if (changed) {
+      start = s_new;
+      cnt = pass_resync<GLOBAL>(cells, ncell, lo, hi, start, t, bm, cnt_a, end_a, end, st_r);
+    }
+  }
+  pf.mark(2);
+  uint32_t inc = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(inc, d);
+    if (lane >= d) inc += v;
+  }
+  const uint32_t off = inc - cnt;
+  if (cnt && off + cnt <= nsym) pass_emit<GLOBAL>(cells, ncell, start, hi, t, outs + off, st_e);
+  pf.mark(3);
+  pf.add_max(8, st_a);
+  pf.add_max(9, st_r);
+  pf.add_max(10, st_e);
+  pf.add(11, (uint32_t)it);
+  pf.add(12, GLOBAL ? 1u : 0u);
+  pf.add(13, 1u);
+}
+
+__global__ void __launch_bounds__(64 * kDecWaves) k_hf_decode(HfDecodeArgs a, int cellcap)
+{
+  extern __shared__ __attribute__((aligned(16))) uint32_t dsm[];
+  __shared__ __attribute__((aligned(16))) uint32_t s_l1[kL1];
+  __shared__ __attribute__((aligned(16))) uint32_t s_l2[kL2Cap];
+  __shared__ uint32_t s_base[32];
+  __shared__ uint16_t s_keys[kMaxBklen];
+  HfTables tb;
+  load_tables(a, s_l1, s_l2, s_base, s_keys, tb);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t* cells = dsm + wid * (cellcap + (((a.sublen + 1) >> 1) + 3) / 4 * 4);
+  uint16_t* outs = reinterpret_cast<uint16_t*>(cells + cellcap);
+
+  DecProf pf;
+  pf.start();
+  for (int c = blockIdx.x * kDecWaves + wid; c < a.pardeg; c += gridDim.x * kDecWaves) {
+    const size_t obase = (size_t)c * a.sublen;
+    if (obase >= a.n) break;
+    const uint32_t nsym = (uint32_t)((a.n - obase) < (size_t)a.sublen ? (a.n - obase) : (size_t)a.sublen);
+    const uint32_t nbit = a.par_nbit[c];
+    const uint32_t ncell = (nbit + 31) >> 5;
+    const uint32_t* src = a.bitstream + a.par_entry[c];
+    if (ncell + 2 <= (uint32_t)cellcap) {
+      for (uint32_t i = lane; i < ncell; i += 64) cells[i] = src[i];
+      if (lane < 2) cells[ncell + lane] = 0;
+      wave_sync();
+      pf.mark(0);
+      decode_chunk<false>(cells, ncell, nbit, nsym, tb, outs, lane, pf);
+    }
+    else {  // a chunk too big for the staging area: read its cells from global memory
+      pf.mark(0);
+      decode_chunk<true>(src, ncell, nbit, nsym, tb, outs, lane, pf);
+    }
+    wave_sync();
+    uint16_t* dst = a.out + obase;
+    const uint32_t n8 = (obase & 7) ? 0u : nsym >> 3;  // 16-B stores only when aligned
+    for (uint32_t i = lane; i < n8; i += 64) reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(outs)[i];
+    for (uint32_t i = (n8 << 3) + lane; i < nsym; i += 64) dst[i] = outs[i];
+    wave_sync();
+    pf.mark(4);
+  }
+#ifdef CUSZ_AMD_DEC_PROFILE
+  const unsigned gw = blockIdx.x * kDecWaves + wid;
+  if (lane == 0 && gw < 4096)
+    for (int k = 0; k < 16; k++) g_dec_prof[gw * 16 + k] = pf.v[k];
+#endif
 }
 
 }  // namespace
@@ -359,8 +876,13 @@ static int enc_group(int sublen, int& cellcap)
   return G;
 }
 
+static bool enc_wave(int sublen) { return sublen % 64 == 0; }
+
+static int enc_wave_cellcap(int sublen) { return ((sublen * kLmax / 32 + 2) + 3) / 4 * 4; }
+
 int hf_encode_groups(int sublen, int pardeg)
 {
+  if (enc_wave(sublen)) return (pardeg + kEncW - 1) / kEncW;
   int cellcap;
   const int G = enc_group(sublen, cellcap);
   return (pardeg + G - 1) / G;
@@ -368,6 +890,13 @@ int hf_encode_groups(int sublen, int pardeg)
 
 int launch_hf_encode(const HfEncodeArgs& a, hipStream_t st)
 {
+  if (enc_wave(a.sublen)) {
+    const int cellcap = enc_wave_cellcap(a.sublen);
+    const int ngroups = (a.pardeg + kEncW - 1) / kEncW;
+    const size_t lds = (size_t)(((a.bklen + 3) & ~3) + kEncW * cellcap) * 4;
+    k_hf_encode_w<<<ngroups, 64 * kEncW, lds, st>>>(a, cellcap);
+    return (int)hipGetLastError();
+  }
   int cellcap;
   const int G = enc_group(a.sublen, cellcap);
   const int ngroups = (a.pardeg + G - 1) / G;
@@ -378,9 +907,56 @@ int launch_hf_encode(const HfEncodeArgs& a, hipStream_t st)
 
 int launch_hf_decode(const HfDecodeArgs& a, hipStream_t st)
 {
-  const int grid = (a.pardeg + 255) / 256;
-  k_hf_decode<<<grid, 256, 0, st>>>(a);
+  if (a.bklen < 1 || a.bklen > kMaxBklen || a.sublen < 1) return (int)hipErrorInvalidValue;
+  k_hf_tables<<<1, 1024, 0, st>>>(a.revbook, a.bklen, a.lut);
+  if (a.pardeg <= 0) return (int)hipGetLastError();
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
+  }
+  // Many chunks: one lane per chunk (every codeword decoded once).  Few long chunks: one wave
+  // per chunk (three passes, but 64-way parallel inside a chunk).
+  const bool lane = a.sublen % 16 == 0 && (a.decoder == 1 || (a.decoder == 0 && a.pardeg >= 64 * ncu));
+  if (lane) {
+    k_hf_decode_lane<<<(a.pardeg + kLpcThreads - 1) / kLpcThreads, kLpcThreads, 0, st>>>(a);
+    return (int)hipGetLastError();
+  }
+  // per wave: staged cells + the chunk's output tile.  The staging area covers the average
+  // chunk with margin; larger chunks read straight from global memory.
+  const int worst = (a.sublen * kLmax / 32 + 4 + 3) / 4 * 4;
+  int cellcap = worst;
+  if (a.avg_cells > 0) {
+    const size_t want = a.avg_cells + a.avg_cells / 2 + 64;
+    cellcap = (int)((want + 15) / 16 * 16);
+    if (cellcap > worst) cellcap = worst;
+  }
+  const size_t lds = ((size_t)cellcap + (((size_t)a.sublen + 1) / 2 + 3) / 4 * 4) * 4 * kDecWaves;
+  if (lds > 120 * 1024) return (int)hipErrorInvalidValue;
+  static int per_cu = 0;
+  static size_t last_lds = 0;
+  if (lds != last_lds) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_hf_decode, 64 * kDecWaves, lds) != hipSuccess ||
+        per_cu < 1)
+      per_cu = 1;
+    last_lds = lds;
+  }
+  const int nblk = (a.pardeg + kDecWaves - 1) / kDecWaves;
+  const int full = per_cu * ncu;
+  const int grid = nblk < full ? nblk : full;
+  k_hf_decode<<<grid, 64 * kDecWaves, lds, st>>>(a, cellcap);
   return (int)hipGetLastError();
 }
+
+#ifdef CUSZ_AMD_DEC_PROFILE
+// copies the per-wave decoder profile of the last decode (u64[4096*16]) to host memory
+extern "C" int psz_amd_debug_decode_profile(unsigned long long* host, int nwords)
+{
+  if (nwords > 4096 * 16) nwords = 4096 * 16;
+  (void)hipDeviceSynchronize();
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dec_prof), (size_t)nwords * 8, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 }  // namespace cusz_amd

@@ -44,6 +44,9 @@ struct HfEncodeArgs {
 };
 int launch_hf_encode(const HfEncodeArgs& a, hipStream_t st);
 
+// decode table scratch (u32 words): L1 4096 | maxl | thresholds | bases | L2 2048
+constexpr int kHfDecTableWords = 4096 + 128 + 2048;
+
 struct HfDecodeArgs {
   const uint32_t* bitstream;
   const uint8_t* revbook;  // first i32[32] | entry i32[32] | keys u16[bklen]
@@ -54,6 +57,9 @@ struct HfDecodeArgs {
   int pardeg;
   size_t n;
   uint16_t* out;
+  uint32_t* lut;     // scratch u32[kHfDecTableWords], 16-B aligned (built by the decode launch)
+  size_t avg_cells;  // average cells per chunk (sizes the LDS staging area); 0 = unknown
+  int decoder;       // PSZ_AMD_DECODER_* (0 auto)
 };
 int launch_hf_decode(const HfDecodeArgs& a, hipStream_t st);
 

@@ -48,15 +48,20 @@ static int ndim_of(psz_len l)
   return 3;
 }
 
+// Chunk length (vle_sublen).  The reference sizes chunks for one encode thread per chunk on
+// maxThreadsPerBlock * nSM / 4 threads (libphf.cc:26-70, which notes "ROCm GPUs should use
+// different constants").  Here the decoder is the consumer that needs the parallelism: one lane
+// per chunk, two waves per SIMD -> nCU * 4 SIMDs * 64 lanes * 2 chunks (131,072 on MI355X, so
+// 512^3 gets sublen 1024, the reference's own HFR setting, hf_buf.cc:77).  Multiple of 256,
+// at most 8192 (encoder LDS); any value is readable by either decoder.
 static void tune_chunking(size_t n, int device, int* sublen, int* pardeg)
-{  // libphf.cc:26-70, evaluated on the caller's device (reference forces device 0)
-  int ncu = 256, maxthr = 1024;
-  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 256;
-  if (hipDeviceGetAttribute(&maxthr, hipDeviceAttributeMaxThreadsPerBlock, device) != hipSuccess) maxthr = 1024;
-  const size_t nthread = (size_t)maxthr * (size_t)ncu / 4;
-  size_t s = (std::max<size_t>(n, 1) - 1) / nthread + 1;
+{
+  int ncu = 256;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1) ncu = 256;
+  const size_t lanes = (size_t)ncu * 4 * 64 * 2;
+  size_t s = (std::max<size_t>(n, 1) - 1) / lanes + 1;
   s = ((s - 1) / 256 + 1) * 256;
-  if (s > 8192) s = 8192;  // encoder limit (LDS cell buffer); format allows any sublen
+  if (s > 8192) s = 8192;
   *sublen = (int)s;
   *pardeg = (int)((std::max<size_t>(n, 1) - 1) / s + 1);
 }
@@ -73,6 +78,7 @@ struct Pipeline {
   LorenzoGeom geom{};
   int sublen = 256, pardeg = 1;
   int user_sublen = 0;
+  int decoder = 0;  // PSZ_AMD_DECODER_*
   uint32_t cap_per_brick = 0, spill_cap = 0;
   size_t splen = 0;
 
@@ -109,7 +115,8 @@ struct Pipeline {
   CompressInfo* info() { return reinterpret_cast<CompressInfo*>(d_small + 64); }
   double* minmax() { return reinterpret_cast<double*>(d_small + 256); }
   unsigned int* ext_scratch() { return reinterpret_cast<unsigned int*>(d_small + 512); }
-  static constexpr size_t kSmallBytes = 512 + 2 * 1024 * 8;
+  uint32_t* dec_lut() { return reinterpret_cast<uint32_t*>(d_small + 512 + 2 * 1024 * 8); }
+  static constexpr size_t kSmallBytes = 512 + 2 * 1024 * 8 + kHfDecTableWords * 4;
 
   ~Pipeline() { release(); }
 
@@ -350,7 +357,14 @@ struct Pipeline {
                     sl,
                     pd,
                     n,
-                    d_codes};
+                    d_codes,
+                    dec_lut(),
+                    0,
+                    decoder};
+    // average chunk size from the segment length (sizes the decoder's LDS staging)
+    const size_t seg = h->entry[PSZHEADER_ENCODED + 1] - h->entry[PSZHEADER_ENCODED];
+    const size_t fixed = 128 + rvbk + 8 * (size_t)pd;
+    if (pd > 0 && seg > fixed) da.avg_cells = (seg - fixed) / 4 / (size_t)pd;
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_hf_decode(da, stream));
     return PSZ_SUCCESS;
   }
@@ -585,6 +599,14 @@ int psz_amd_set_sublen(psz_resource* m, int sublen)
     cusz_amd::tune_chunking(p->n, p->device, &p->sublen, &p->pardeg);
     if (p->alloc_chunk_state() != hipSuccess) return PSZ_ABORT_NOT_IMPLEMENTED;
   }
+  return PSZ_SUCCESS;
+}
+
+int psz_amd_set_decoder(psz_resource* m, int kind)
+{
+  Pipeline* p = cusz_amd::P(m);
+  if (!p || kind < PSZ_AMD_DECODER_AUTO || kind > PSZ_AMD_DECODER_WAVE) return PSZ_ABORT_NOT_IMPLEMENTED;
+  p->decoder = kind;
   return PSZ_SUCCESS;
 }
 

@@ -50,13 +50,20 @@ int psz_amd_enable_timing(psz_resource* m, int on);
 int psz_amd_stage_times(psz_resource* m, float* ms, int n);
 
 /* Override the Huffman chunk length (symbols per chunk, rounded up to a multiple of 256,
- * at most 8192) used by the next compress; 0 restores cuSZ's tuning rule
- * (libphf.cc:26-70 evaluated on the current device). */
+ * at most 8192) used by the next compress; 0 restores the default (nCU * 512 chunks, see
+ * DESIGN.md; the reference's libphf.cc:26-70 rule targets one encode thread per chunk). */
 int psz_amd_set_sublen(psz_resource* m, int sublen);
 
 /* Decode-only entry point used by the multi-GPU gather path and tests: decodes the Huffman
  * segment of a device archive into the manager's code buffer. */
 int psz_amd_decode_codes(psz_resource* m, uint8_t* IN_d_compressed);
+
+/* Huffman decoder selection: 0 auto (default), 1 one lane per chunk, 2 one wave per chunk.
+ * Both decode the same archives bit-exactly; tests exercise both. */
+#define PSZ_AMD_DECODER_AUTO 0
+#define PSZ_AMD_DECODER_LANE 1
+#define PSZ_AMD_DECODER_WAVE 2
+int psz_amd_set_decoder(psz_resource* m, int kind);
 
 const char* psz_amd_version(void);
 

@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Decoder phase profile (diagnostic): loads the instrumented library (make -C cusz_amd prof),
+compresses + decompresses one field and prints per-chunk cycle/step averages per wave."""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("CUSZ_AMD_LIB", os.path.join(ROOT, "cusz_amd", "lib_prof", "libcusz_amd.so"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import cusz_amd as cz  # noqa: E402
+from cusz_amd import datagen  # noqa: E402
+
+dims = tuple(int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "512x512x512").split("x"))
+eb = float(sys.argv[2]) if len(sys.argv) > 2 else 1e-4
+torch.cuda.set_device(0)
+dev = torch.device("cuda", 0)
+x = datagen.smooth3d_torch(dims, seed=2, device=dev)
+y = torch.empty_like(x)
+s = torch.cuda.current_stream(dev)
+r = cz.Resource(cz.F4, dims, stream=s.cuda_stream)
+r.enable_timing(True)
+for _ in range(3):
+    ptr, nb, _ = r.compress(x.data_ptr(), eb, cz.Abs)
+    r.decompress(ptr, nb, y.data_ptr())
+torch.cuda.synchronize()
+L = cz.lib()
+buf = (C.c_ulonglong * (4096 * 16))()
+L.psz_amd_debug_decode_profile(buf, 4096 * 16)
+a = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 16).astype(np.float64)
+a = a[a[:, 13] > 0]
+ch = a[:, 13].sum()
+names = ["stage", "passA", "fixup", "emit", "write"]
+tot = a[:, :5].sum()
+print(f"waves={len(a)} chunks={int(ch)} chunks/wave={ch/len(a):.1f} decode_ms={r.stage_times()[cz.T_DECODE]:.4f}")
+for k, nm in enumerate(names):
+    print(f"  {nm:6s} cycles/chunk={a[:, k].sum()/ch:9.0f}  share={a[:, k].sum()/tot:.3f}")
+print(f"  wave-steps/chunk passA={a[:,8].sum()/ch:.1f} resync={a[:,9].sum()/ch:.1f} emit={a[:,10].sum()/ch:.1f}"
+      f" fix-iters/chunk={a[:,11].sum()/ch:.2f} global-path chunks={int(a[:,12].sum())}")
+print(f"  per-wave total cycles: min={a[:, :5].sum(1).min():.0f} max={a[:, :5].sum(1).max():.0f}")

@@ -1,7 +1,7 @@
 #!/bin/bash
-# Runs GPU steps in order; each has its own time limit. Stops at the first step that
-# faults, aborts, segfaults or times out (exit 124/134/137/139 or >128); ordinary test
-# failures (exit 1) do not stop later steps.  Usage: scripts/gpu_job.sh "name:secs:cmd" ...
+# Runs GPU steps in order; each has its own time limit. Stops at the first step that fails
+# in any way (a failed test may be a GPU fault: nothing more runs on the card after it).
+# Usage: scripts/gpu_job.sh "name:secs:cmd" ...
 mkdir -p gpurun_out
 for spec in "$@"; do
   name="${spec%%:*}"; rest="${spec#*:}"; secs="${rest%%:*}"; cmd="${rest#*:}"
@@ -10,6 +10,6 @@ for spec in "$@"; do
   rc=$?
   echo "=== [$name] rc=$rc $(date +%T)" | tee -a gpurun_out/job.log
   tail -3 "gpurun_out/$name.log" | tee -a gpurun_out/job.log
-  if [ $rc -ge 124 ]; then echo "stopping after fatal rc=$rc" | tee -a gpurun_out/job.log; exit $rc; fi
+  if [ $rc -ne 0 ]; then echo "stopping after rc=$rc" | tee -a gpurun_out/job.log; exit $rc; fi
 done
 exit 0

@@ -1,0 +1,7 @@
+#!/bin/bash
+# Quick GPU pass: parity tests, bench, kernel-trace stats (run through gpurun from the repo root).
+export TMPDIR=/tmp
+exec scripts/gpu_job.sh \
+  "parity:400:python -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py tests -q -m gpu --timeout 250 -p no:cacheprovider -x" \
+  "bench:300:python bench.py --steps 10 --warmup 3 ${BENCH_ARGS:---no-cpu-baseline}" \
+  "stats:300:rocprofv3 --kernel-trace --stats -d gpurun_out/prof_stats -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --profile-only"

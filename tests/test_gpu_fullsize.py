@@ -41,11 +41,15 @@ def _check_full(oracle, d_in, dims, eb, slabs, dtype=np.float32):
         sub = host[z0 * x * y:(z0 + nz) * x * y]
         c_o, _, _ = oracle.lorenzo_c(sub, (x, y, nz), eb)
         np.testing.assert_array_equal(codes_h[z0 * x * y:(z0 + nz) * x * y], c_o)
-    # (b) decode(encode) idempotence through the archive
-    r.decode_codes(ptr)
-    sync()
-    dec = d2h(ino.d_quant_codes, 2 * n, np.uint16)
-    np.testing.assert_array_equal(dec, codes_h)
+    # (b) decode(encode) idempotence through the archive, with both decoders
+    for kind in (cz.DECODER_LANE, cz.DECODER_WAVE, cz.DECODER_AUTO):
+        r.set_decoder(kind)
+        codes_t.zero_()
+        assert hip().hipMemcpy(C.c_void_p(ino.d_quant_codes), C.c_void_p(codes_t.data_ptr()), 2 * n, 3) == 0
+        r.decode_codes(ptr)
+        sync()
+        dec = d2h(ino.d_quant_codes, 2 * n, np.uint16)
+        np.testing.assert_array_equal(dec, codes_h, err_msg=f"decoder {kind}")
     # (c) error bound after a full decompress into a poisoned buffer
     out = empty_device(n, torch.float32 if dtype == np.float32 else torch.float64)
     out.fill_(float("nan"))

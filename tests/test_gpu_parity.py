@@ -72,21 +72,29 @@ def run_roundtrip(oracle, data, dims, eb, dtype=np.float32, zigzag=False, radius
     np.testing.assert_array_equal(a["bitstream"], info["bitstream"])
     assert a["phf"] == seg_o, "phf segment bytes differ"
 
-    # ---- stage 3: decompress into an un-zeroed, NaN-poisoned buffer -----------------------
-    out = empty_device(n, getattr(torch, tdt))
-    out.fill_(float("nan"))
-    r.decompress(ptr, nbytes, out.data_ptr())
-    sync()
-    xg = out.cpu().numpy()
+    # ---- stage 3: decompress into an un-zeroed, NaN-poisoned buffer, with each decoder -----
     xo = oracle.lorenzo_x(codes_o, ov_o, oi_o, dims, eb, radius, zigzag, dtype)
-    bad = np.flatnonzero(xg.view(np.uint64 if dtype == np.float64 else np.uint32) != xo.view(np.uint64 if dtype == np.float64 else np.uint32))
-    assert bad.size == 0, f"{bad.size} reconstruction mismatches, first {bad[:5]}: {xg[bad[:5]]} vs {xo[bad[:5]]}"
+    ubits = np.uint64 if dtype == np.float64 else np.uint32
+    for dec in DECODERS:
+        r.set_decoder(dec)
+        out = empty_device(n, getattr(torch, tdt))
+        out.fill_(float("nan"))
+        r.decompress(ptr, nbytes, out.data_ptr())
+        sync()
+        xg = out.cpu().numpy()
+        bad = np.flatnonzero(xg.view(ubits) != xo.view(ubits))
+        assert bad.size == 0, f"decoder {dec}: {bad.size} reconstruction mismatches, first {bad[:5]}: " \
+                              f"{xg[bad[:5]]} vs {xo[bad[:5]]}"
+    r.set_decoder(cz.DECODER_AUTO)
     if check_bound:  # f32/f64 prequant rounding adds a few ulp of |x| (same in the reference)
         tol = 1.001 * eb + 4 * float(np.spacing(np.abs(data).max().astype(dtype)))
         assert np.max(np.abs(xg.astype(np.float64) - data)) <= tol
     r.close()
     return arch, a
 
+
+# auto, one lane per chunk, one wave per chunk (PSZ_AMD_DECODER_*)
+DECODERS = (cz.DECODER_AUTO, cz.DECODER_LANE, cz.DECODER_WAVE)
 
 CASES = [
     # (kind, dims, dtype, eb, zigzag, radius)
