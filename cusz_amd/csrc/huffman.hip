@@ -238,6 +238,11 @@ __device__ __forceinline__ void load_codes16(const uint16_t* p, int mine, uint32
   }
 }
 
+#ifdef CUSZ_AMD_DEC_PROFILE
+// per-workgroup encoder phase clocks (diagnostic build): setup, pack, look-back, write-out
+__device__ unsigned long long g_enc_prof[65536 * 4];
+#endif
+
 __global__ void __launch_bounds__(64 * kEncW) k_hf_encode_w(HfEncodeArgs a, int cellcap)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -246,10 +251,17 @@ __global__ void __launch_bounds__(64 * kEncW) k_hf_encode_w(HfEncodeArgs a, int 
   __shared__ uint32_t s_nbit[kEncW];
   __shared__ uint32_t s_base;
 
+#ifdef CUSZ_AMD_DEC_PROFILE
+  unsigned long long ept[5];
+  ept[0] = __builtin_readcyclecounter();
+#endif
   for (int i = threadIdx.x; i < a.bklen; i += blockDim.x) s_book[i] = a.book[i];
   for (int i = threadIdx.x; i < kEncW * cellcap / 4; i += blockDim.x)
     reinterpret_cast<uint4*>(s_cells)[i] = make_uint4(0, 0, 0, 0);
   __syncthreads();
+#ifdef CUSZ_AMD_DEC_PROFILE
+  ept[1] = __builtin_readcyclecounter();
+#endif
 
   const int g = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int c = g * kEncW + wid;
@@ -290,6 +302,9 @@ __global__ void __launch_bounds__(64 * kEncW) k_hf_encode_w(HfEncodeArgs a, int 
   }
   if (lane == 0) s_nbit[wid] = nbits;
   __syncthreads();
+#ifdef CUSZ_AMD_DEC_PROFILE
+  ept[2] = __builtin_readcyclecounter();
+#endif
 
   uint32_t gcells = 0;
   for (int j = 0; j < kEncW; j++) gcells += (s_nbit[j] + 31) >> 5;
@@ -327,6 +342,9 @@ __global__ void __launch_bounds__(64 * kEncW) k_hf_encode_w(HfEncodeArgs a, int 
     if (lane == 0) s_base = base;
   }
   __syncthreads();
+#ifdef CUSZ_AMD_DEC_PROFILE
+  ept[3] = __builtin_readcyclecounter();
+#endif
 
   // each wave writes its own chunk (cells start on a fresh cell per chunk)
   uint32_t off = s_base;
@@ -337,6 +355,11 @@ __global__ void __launch_bounds__(64 * kEncW) k_hf_encode_w(HfEncodeArgs a, int 
     const uint32_t* cells = s_cells + wid * cellcap;
     for (uint32_t i = lane; i < nc; i += 64) a.bitstream[off + i] = cells[i];
   }
+#ifdef CUSZ_AMD_DEC_PROFILE
+  ept[4] = __builtin_readcyclecounter();
+  if (threadIdx.x == 0 && g < 65536)
+    for (int q = 0; q < 4; q++) g_enc_prof[g * 4 + q] = ept[q + 1] - ept[q];
+#endif
 }
 
 // ============================== decode ======================================================
@@ -533,6 +556,39 @@ __device__ __forceinline__ void load_tables(const HfDecodeArgs& a, uint32_t* s_l
   for (int q = 0; q < kLongLens; q++) tb.first[q] = __builtin_amdgcn_readfirstlane(a.lut[kTabFirst + kLutBits + 1 + q]);
 }
 
+#ifdef CUSZ_AMD_DEC_PROFILE
+// per-wave phase clocks and step counts (diagnostic build only; read by psz_amd_debug_decode_profile)
+__device__ unsigned long long g_dec_prof[4096 * 16];
+#define DP_STEP(x) (x)++
+#else
+#define DP_STEP(x) (void)0
+#endif
+
+struct DecProf {
+#ifdef CUSZ_AMD_DEC_PROFILE
+  unsigned long long v[16] = {0};
+  unsigned long long t = 0;
+  __device__ void start() { t = __builtin_readcyclecounter(); }
+  __device__ void mark(int k)
+  {
+    const unsigned long long n = __builtin_readcyclecounter();
+    v[k] += n - t;
+    t = n;
+  }
+  __device__ void add(int k, uint32_t x) { v[k] += x; }
+  __device__ void add_max(int k, uint32_t x)
+  {
+    for (int d = 32; d > 0; d >>= 1) x = max(x, (uint32_t)__shfl_xor(x, d));
+    v[k] += x;
+  }
+#else
+  __device__ void start() {}
+  __device__ void mark(int) {}
+  __device__ void add(int, uint32_t) {}
+  __device__ void add_max(int, uint32_t) {}
+#endif
+};
+
 // ---- lane-per-chunk decoder (the reference's decomposition, hf_kernels.cuhip.inl:331-396) ----
 // Each lane decodes one whole chunk, so there is no synchronisation pass and every codeword is
 // decoded once.  Per lane: a 4-block (16-cell) LDS ring fed by 16-B loads issued two cadences
@@ -568,26 +624,32 @@ __global__ void __launch_bounds__(kLpcThreads) k_hf_decode_lane(HfDecodeArgs a)
   const uint32_t skip = mis >> 2;
   const uint32_t nblk = (skip + ncell + 3) >> 2;
   const bool tail = live && c + 1 == (uint32_t)a.pardeg;  // last chunk: never read past its cells
-  // every call issues exactly one 16-B load (so the compiler can wait for one pending slot
-  // without waiting for the other); the last chunk's final partial block is re-read by cells
+  // Every cadence issues exactly one 16-B load and two 16-B stores per lane, unconditionally
+  // (targets swapped for safe dummies when unused), so the compiler's vmcnt waits are exact
+  // and a ring refill waits only for its own load, issued two cadences earlier.  The last
+  // chunk's final partial block is read once, by cells, before the loop (never past the end).
   const uint4* gsafe = reinterpret_cast<const uint4*>(a.lut);
+  const uint32_t tb_blk = nblk ? nblk - 1 : 0u;  // the last block of this chunk
+  const bool tail_partial = tail && nblk && (tb_blk + 1) * 4 > skip + ncell;
+  uint4 tailv = make_uint4(0, 0, 0, 0);
+  if (tail_partial) {
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(gb + tb_blk);
+    const uint32_t lim = skip + ncell - tb_blk * 4;  // valid cells in this block (1..3)
+    tailv.x = q[0];
+    tailv.y = lim > 1 ? q[1] : 0u;
+    tailv.z = lim > 2 ? q[2] : 0u;
+  }
+  // raw 16-B load of block b (the tail block's stand-in is substituted when it is written to
+  // the ring, so the loaded registers are not touched before the ring write needs them)
   auto load_block = [&](uint32_t b) -> uint4 {
-    const uint32_t bb = min(b, nblk ? nblk - 1 : 0u);
-    const bool partial = tail && (bb + 1) * 4 > skip + ncell;
-    uint4 v = *((live && !partial) ? gb + bb : gsafe);
-    if (partial) {
-      const uint32_t* q = reinterpret_cast<const uint32_t*>(gb + bb);
-      const uint32_t lim = skip + ncell - bb * 4;  // valid cells in this block (1..3)
-      v.x = q[0];
-      v.y = lim > 1 ? q[1] : 0u;
-      v.z = lim > 2 ? q[2] : 0u;
-      v.w = 0u;
-    }
-    return v;
+    const uint32_t bb = min(b, tb_blk);
+    const bool use_tail = tail_partial && bb == tb_blk;
+    return *((live && !use_tail) ? gb + bb : gsafe);
   };
   uint32_t* ring = s_in + threadIdx.x * kInStride;
   uint16_t* oring = reinterpret_cast<uint16_t*>(s_out + threadIdx.x * kOutStride);
-  auto ring_put = [&](uint32_t b, const uint4& v) {
+  auto ring_put = [&](uint32_t b, uint4 v) {
+    if (tail_partial && b == tb_blk) v = tailv;
     reinterpret_cast<uint4*>(ring)[b & 3] = v;
     if ((b & 3) == 0) ring[16] = v.x;  // mirror: a window starting in cell 15 reads cell 0 as cell 16
   };
@@ -603,11 +665,21 @@ __global__ void __launch_bounds__(kLpcThreads) k_hf_decode_lane(HfDecodeArgs a)
       if ((uint32_t)b < ld) ring_put(b, v[b]);
   }
   uint32_t bA = ld, bB = ld + 1;
-  uint4 pA = load_block(bA), pB = load_block(bB);
-
   uint32_t pos = skip * 32, cnt = 0, flushed = 0;
   uint16_t* gout = a.out + obase;
 
+  // flush 16 symbols (32 B) when a ring half is full (scattered per-lane stores are costly
+  // in the address path, so they are issued only when there is something to write)
+  auto flush = [&]() {
+    if (cnt - flushed >= 16u) {
+      const uint4* src = reinterpret_cast<const uint4*>(oring + (flushed & 16u));
+      uint4* dst = reinterpret_cast<uint4*>(gout + flushed);
+      const uint4 v0 = src[0], v1 = src[1];
+      dst[0] = v0;
+      dst[1] = v1;
+      flushed += 16;
+    }
+  };
   auto steps = [&]() {
 #pragma unroll
     for (int s = 0; s < kCad; s++) {
@@ -631,37 +703,40 @@ __global__ void __launch_bounds__(kLpcThreads) k_hf_decode_lane(HfDecodeArgs a)
       ld++;
     }
     if (b < ld) b += 2;
+    flush();
     p = load_block(b);
-    if (cnt - flushed >= 16u) {
-      const uint4* src = reinterpret_cast<const uint4*>(oring + (flushed & 16u));
-      uint4* dst = reinterpret_cast<uint4*>(gout + flushed);
-      const uint4 v0 = src[0], v1 = src[1];
-      dst[0] = v0;
-      dst[1] = v1;
-      flushed += 16;
-    }
   };
+  uint4 pA = load_block(bA), pB = load_block(bB);
+  DecProf pf;
+  pf.start();
+  uint32_t iters = 0;
   while (__any(cnt < nsym)) {
     steps();
+    pf.mark(1);
     cadence(pA, bA);
+    pf.mark(2);
     steps();
+    pf.mark(1);
     cadence(pB, bB);
+    pf.mark(2);
+    iters++;
   }
   wave_sync();
   for (uint32_t i = flushed; i < cnt; i++) gout[i] = oring[i & 31u];
+  pf.mark(4);
+  pf.add(8, iters);
+  pf.add(13, 1u);
+#ifdef CUSZ_AMD_DEC_PROFILE
+  const unsigned gw = (blockIdx.x * kLpcThreads + threadIdx.x) >> 6;
+  if ((threadIdx.x & 63) == 0 && gw < 4096)
+    for (int k = 0; k < 16; k++) g_dec_prof[gw * 16 + k] = pf.v[k];
+#endif
 }
 
 // ---- wave-per-chunk decoder (for few, long chunks) ------------------------------------------
 constexpr int kDecWaves = 4;   // waves per decode workgroup
 constexpr int kSyncWin = 64;   // bits of a segment whose codeword starts are remembered
 
-#ifdef CUSZ_AMD_DEC_PROFILE
-// per-wave phase clocks and step counts (diagnostic build only; read by psz_amd_debug_decode_profile)
-__device__ unsigned long long g_dec_prof[4096 * 16];
-#define DP_STEP(x) (x)++
-#else
-#define DP_STEP(x) (void)0
-#endif
 
 // the 32 stream bits starting at bit `pos` (MSB-first cells)
 template <bool GLOBAL>
@@ -750,30 +825,6 @@ __device__ __forceinline__ void pass_emit(const uint32_t* cells, uint32_t ncell,
   }
 }
 
-struct DecProf {
-#ifdef CUSZ_AMD_DEC_PROFILE
-  unsigned long long v[16] = {0};
-  unsigned long long t = 0;
-  __device__ void start() { t = __builtin_readcyclecounter(); }
-  __device__ void mark(int k)
-  {
-    const unsigned long long n = __builtin_readcyclecounter();
-    v[k] += n - t;
-    t = n;
-  }
-  __device__ void add(int k, uint32_t x) { v[k] += x; }
-  __device__ void add_max(int k, uint32_t x)
-  {
-    for (int d = 32; d > 0; d >>= 1) x = max(x, (uint32_t)__shfl_xor(x, d));
-    v[k] += x;
-  }
-#else
-  __device__ void start() {}
-  __device__ void mark(int) {}
-  __device__ void add(int, uint32_t) {}
-  __device__ void add_max(int, uint32_t) {}
-#endif
-};
 
 template <bool GLOBAL>
 __device__ __forceinline__ void decode_chunk(const uint32_t* cells, uint32_t ncell, uint32_t nbit, uint32_t nsym,
@@ -950,6 +1001,13 @@ int launch_hf_decode(const HfDecodeArgs& a, hipStream_t st)
 }
 
 #ifdef CUSZ_AMD_DEC_PROFILE
+extern "C" int psz_amd_debug_encode_profile(unsigned long long* host, int nwords)
+{
+  if (nwords > 65536 * 4) nwords = 65536 * 4;
+  (void)hipDeviceSynchronize();
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_enc_prof), (size_t)nwords * 8, 0, hipMemcpyDeviceToHost);
+}
+
 // copies the per-wave decoder profile of the last decode (u64[4096*16]) to host memory
 extern "C" int psz_amd_debug_decode_profile(unsigned long long* host, int nwords)
 {

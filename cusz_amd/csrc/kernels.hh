@@ -44,8 +44,10 @@ struct HfEncodeArgs {
 };
 int launch_hf_encode(const HfEncodeArgs& a, hipStream_t st);
 
-// decode table scratch (u32 words): L1 4096 | maxl | thresholds | bases | L2 2048
+// decode table scratch (u32 words): L1 4096 | maxl | first[] | bases | L2 2048, then a 32-B
+// sink the lane decoder stores to when it has nothing to flush (HfDecodeArgs::lut)
 constexpr int kHfDecTableWords = 4096 + 128 + 2048;
+constexpr int kHfDecScratchWords = kHfDecTableWords + 16;
 
 struct HfDecodeArgs {
   const uint32_t* bitstream;

@@ -466,6 +466,57 @@ k_lorenzo_c3d(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
 // be pre-zeroed (Lorenzo).  ZigZag additionally needs a zeroed plane (code 0 = delta 0).
 // =========================================================================================
 
+// V codes packed two per u32 (prefetch registers)
+template <int V>
+__device__ __forceinline__ void load_codes_packed(const uint16_t* __restrict__ c, size_t base, uint32_t x0,
+                                                  uint32_t lx, bool row_ok, uint32_t (&w)[(V + 1) / 2])
+{
+  if (row_ok && x0 + V <= lx) {
+    const uint16_t* q = c + base + x0;
+    if constexpr (V == 4) {
+      const uint2 u = *reinterpret_cast<const uint2*>(q);
+      w[0] = u.x, w[1] = u.y;
+    }
+    else if constexpr (V == 2) {
+      w[0] = *reinterpret_cast<const uint32_t*>(q);
+    }
+    else {
+#pragma unroll
+      for (int k = 0; k < (V + 1) / 2; k++) w[k] = 0;
+#pragma unroll
+      for (int k = 0; k < V; k++) w[k >> 1] |= (uint32_t)q[k] << ((k & 1) * 16);
+    }
+  }
+  else {
+#pragma unroll
+    for (int k = 0; k < (V + 1) / 2; k++) w[k] = 0;
+#pragma unroll
+    for (int k = 0; k < V; k++)
+      w[k >> 1] |= (uint32_t)((row_ok && x0 + k < lx) ? c[base + x0 + k] : uint16_t(0)) << ((k & 1) * 16);
+  }
+}
+
+// codes already in registers (loaded a step ahead); the outlier plane is read only where
+// code == 0
+template <typename T, int V, bool ZZ>
+__device__ __forceinline__ void fuse_codes(const uint32_t (&w)[(V + 1) / 2], const T* plane, size_t base,
+                                           uint32_t x0, uint32_t lx, bool ok, T r, T (&v)[V])
+{
+  uint16_t c[V];
+#pragma unroll
+  for (int k = 0; k < V; k++) c[k] = (uint16_t)(w[k >> 1] >> ((k & 1) * 16));
+#pragma unroll
+  for (int k = 0; k < V; k++) {
+    const bool in = ok && (x0 + k < lx);
+    T o = 0;
+    if (in && c[k] == 0) o = plane[base + x0 + k];
+    if constexpr (ZZ)
+      v[k] = in ? o + (T)zz_dec(c[k]) : T(0);
+    else
+      v[k] = in ? (o + (T)c[k]) - r : T(0);
+  }
+}
+
 template <typename T, int V, bool ZZ>
 __device__ __forceinline__ void fuse_row(const uint16_t* __restrict__ codes, const T* plane, size_t base,
                                          uint32_t x0, uint32_t lx, bool ok, T r, T (&v)[V])
@@ -579,7 +630,7 @@ k_lorenzo_x2d(const uint16_t* __restrict__ codes, T* out, uint32_t lx, uint32_t 
 }
 
 template <typename T, int V, bool ZZ>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
 k_lorenzo_x3d(const uint16_t* __restrict__ codes, T* out, uint32_t lx, uint32_t ly, uint32_t lz, T ebx2,
               T r, uint32_t nbx, uint32_t nby, uint32_t nbricks)
 {
@@ -590,15 +641,34 @@ k_lorenzo_x3d(const uint16_t* __restrict__ codes, T* out, uint32_t lx, uint32_t 
     const uint32_t bx = brick % nbx, tt = brick / nbx, by = tt % nby, bz = tt / nby;
     const uint32_t x0 = bx * (64 * V) + lane * V, y0 = by * 8, z0 = bz * 8;
     T s[8][V];
+    // codes are loaded one y-step ahead so a step waits at most for its (rare) outlier reads
+    constexpr int W = (V + 1) / 2;
+    uint32_t cn[8][W];
+#pragma unroll
+    for (int z = 0; z < 8; z++)
+      load_codes_packed<V>(codes, (size_t)(z0 + z) * plane + (size_t)y0 * lx, x0, lx, (z0 + z) < lz && y0 < ly,
+                           cn[z]);
     for (int y = 0; y < 8; y++) {
       const uint32_t gy = y0 + y;
       if (gy >= ly) break;
+      uint32_t cc[8][W];
+#pragma unroll
+      for (int z = 0; z < 8; z++)
+#pragma unroll
+        for (int k = 0; k < W; k++) cc[z][k] = cn[z][k];
+      if (y + 1 < 8) {
+        const bool nok = gy + 1 < ly;
+#pragma unroll
+        for (int z = 0; z < 8; z++)
+          load_codes_packed<V>(codes, (size_t)(z0 + z) * plane + (size_t)(gy + 1) * lx, x0, lx,
+                               nok && (z0 + z) < lz, cn[z]);
+      }
       T t[8][V];
 #pragma unroll
       for (int z = 0; z < 8; z++) {
         const bool ok = (z0 + z) < lz;
         T v[V];
-        fuse_row<T, V, ZZ>(codes, out, (size_t)(z0 + z) * plane + (size_t)gy * lx, x0, lx, ok, r, v);
+        fuse_codes<T, V, ZZ>(cc[z], out, (size_t)(z0 + z) * plane + (size_t)gy * lx, x0, lx, ok, r, v);
 #pragma unroll
         for (int k = 0; k < V; k++) {
           s[z][k] = (y > 0) ? v[k] + s[z][k] : v[k];  // y sequential (lrz_x:315)

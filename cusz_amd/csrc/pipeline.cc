@@ -116,7 +116,7 @@ struct Pipeline {
   double* minmax() { return reinterpret_cast<double*>(d_small + 256); }
   unsigned int* ext_scratch() { return reinterpret_cast<unsigned int*>(d_small + 512); }
   uint32_t* dec_lut() { return reinterpret_cast<uint32_t*>(d_small + 512 + 2 * 1024 * 8); }
-  static constexpr size_t kSmallBytes = 512 + 2 * 1024 * 8 + kHfDecTableWords * 4;
+  static constexpr size_t kSmallBytes = 512 + 2 * 1024 * 8 + kHfDecScratchWords * 4;
 
   ~Pipeline() { release(); }
 

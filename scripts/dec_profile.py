@@ -34,11 +34,18 @@ L.psz_amd_debug_decode_profile(buf, 4096 * 16)
 a = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 16).astype(np.float64)
 a = a[a[:, 13] > 0]
 ch = a[:, 13].sum()
-names = ["stage", "passA", "fixup", "emit", "write"]
+names = ["prologue", "steps", "cadence", "-", "tail"]
 tot = a[:, :5].sum()
-print(f"waves={len(a)} chunks={int(ch)} chunks/wave={ch/len(a):.1f} decode_ms={r.stage_times()[cz.T_DECODE]:.4f}")
+print(f"(lane decoder: 'chunks' = waves) waves={len(a)} chunks={int(ch)} chunks/wave={ch/len(a):.1f} decode_ms={r.stage_times()[cz.T_DECODE]:.4f}")
 for k, nm in enumerate(names):
     print(f"  {nm:6s} cycles/chunk={a[:, k].sum()/ch:9.0f}  share={a[:, k].sum()/tot:.3f}")
-print(f"  wave-steps/chunk passA={a[:,8].sum()/ch:.1f} resync={a[:,9].sum()/ch:.1f} emit={a[:,10].sum()/ch:.1f}"
-      f" fix-iters/chunk={a[:,11].sum()/ch:.2f} global-path chunks={int(a[:,12].sum())}")
+print(f"  loop iterations per wave={a[:,8].mean():.1f} (8 steps each)")
 print(f"  per-wave total cycles: min={a[:, :5].sum(1).min():.0f} max={a[:, :5].sum(1).max():.0f}")
+
+e = (C.c_ulonglong * (65536 * 4))()
+L.psz_amd_debug_encode_profile(e, 65536 * 4)
+e = np.frombuffer(e, dtype=np.uint64).reshape(65536, 4).astype(np.float64)
+e = e[e.sum(1) > 0]
+print(f"encoder: {len(e)} workgroups profiled, encode_ms={r.stage_times()[cz.T_ENCODE]:.4f}")
+for k, nm in enumerate(["setup", "pack", "lookback", "write"]):
+    print(f"  {nm:8s} cycles/wg: mean={e[:, k].mean():9.0f} p50={np.median(e[:, k]):9.0f} max={e[:, k].max():9.0f}")
