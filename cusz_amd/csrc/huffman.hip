@@ -38,13 +38,16 @@ __device__ __forceinline__ void st_status(unsigned long long* p, unsigned long l
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane)
+// inclusive wave64 prefix sum with DPP (row_shr inside 16-lane rows, then row_bcast15/31 across
+// rows): six VALU ops instead of six LDS-routed ds_bpermute round trips
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int /*lane*/)
 {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t t = __shfl_up(v, d);
-    if (lane >= d) v += t;
-  }
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
   return v;
 }
 
@@ -360,6 +363,173 @@ __global__ void __launch_bounds__(64 * kEncW) k_hf_encode_w(HfEncodeArgs a, int 
   if (threadIdx.x == 0 && g < 65536)
     for (int q = 0; q < 4; q++) g_enc_prof[g * 4 + q] = ept[q + 1] - ept[q];
 #endif
+}
+
+// ---- three-phase encoder (default) ------------------------------------------------------------
+// The look-back encoders above serialise workgroups on their predecessors' prefixes; on MI355X
+// that latency, not bandwidth, bounds them.  Here:
+//  (1) k_hf_pack: persistent waves, one chunk per wave at a time, codes prefetched a round
+//      ahead; the chunk's cells go to a scratch slot at a fixed worst-case stride;
+//  (2) k_hf_chunk_scan: one workgroup scans the per-chunk cell counts into par_entry;
+//  (3) k_hf_gather: one wave per chunk copies its cells to their final place (coalesced).
+// The extra 2 x (compressed bytes) of traffic is far cheaper than the look-back chain.
+constexpr int kPackWaves = 4;
+
+__global__ void __launch_bounds__(64 * kPackWaves) k_hf_pack(HfEncodeArgs a, int cellcap)
+{
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint32_t* s_book = smem;                          // bklen words (rounded to 4)
+  uint32_t* s_cells = smem + ((a.bklen + 3) & ~3);  // kPackWaves * cellcap words
+  for (int i = threadIdx.x; i < a.bklen; i += blockDim.x) s_book[i] = a.book[i];
+  for (int i = threadIdx.x; i < kPackWaves * cellcap / 4; i += blockDim.x)
+    reinterpret_cast<uint4*>(s_cells)[i] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int stride = gridDim.x * kPackWaves;
+  const int per = a.sublen / 64 < kRound ? a.sublen / 64 : kRound;  // codes per lane per round
+  const int span = per * 64;
+  const bool vec_ok = per == kRound;
+  uint32_t* cells = s_cells + wid * cellcap;
+  auto chunk_len = [&](int c) -> int {
+    const size_t start = (size_t)c * a.sublen;
+    return (int)((a.n - start) < (size_t)a.sublen ? (a.n - start) : (size_t)a.sublen);
+  };
+  auto load_round = [&](int c, int r0, int cnt, uint32_t(&v)[8]) {
+    const int lo = r0 + lane * per, mine = min(max(cnt - lo, 0), per);
+    load_codes16(a.codes + (size_t)c * a.sublen + lo, mine, v, vec_ok && mine == per);
+  };
+
+  int c = blockIdx.x * kPackWaves + wid;
+  uint32_t nxt[8];
+  if (c < a.pardeg) load_round(c, 0, chunk_len(c), nxt);
+  for (; c < a.pardeg; c += stride) {
+    const int cnt = chunk_len(c);
+    uint32_t nbits = 0;
+    for (int r0 = 0; r0 < cnt; r0 += span) {
+      const int lo = r0 + lane * per, mine = min(max(cnt - lo, 0), per);
+      uint32_t cur[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) cur[i] = nxt[i];
+      if (r0 + span < cnt)  // prefetch: next round of this chunk, or the first of the next chunk
+        load_round(c, r0 + span, cnt, nxt);
+      else if (c + stride < a.pardeg)
+        load_round(c + stride, 0, chunk_len(c + stride), nxt);
+      uint32_t w[kRound], bits = 0;
+#pragma unroll
+      for (int i = 0; i < kRound; i++) {
+        const uint32_t code = (cur[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
+        w[i] = i < mine ? s_book[code] : 0u;
+        bits += w[i] >> 27;
+      }
+      const uint32_t inc = wave_incl_scan(bits, lane);
+      if (mine) pack_words<kRound>(cells, nbits + inc - bits, w, mine);
+      nbits += __shfl(inc, 63);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t nc = (nbits + 31) >> 5;
+    uint32_t* dst = a.temp + (size_t)c * cellcap;
+    for (uint32_t i = lane; i < nc; i += 64) {
+      dst[i] = cells[i];
+      cells[i] = 0u;  // ready for the next chunk
+    }
+    if (lane == 0) a.par_nbit[c] = nbits;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// per-tile cell totals (tile = kGatherTile consecutive chunks), one wave per tile
+constexpr int kGatherTile = 64;
+
+__global__ void __launch_bounds__(256) k_hf_tile_sums(const uint32_t* __restrict__ par_nbit, int pardeg,
+                                                      uint32_t* __restrict__ tile_sum, int ntiles)
+{
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= ntiles) return;
+  uint32_t acc = 0;
+  for (int i = t * kGatherTile + lane; i < min((t + 1) * kGatherTile, pardeg); i += 64) acc += (par_nbit[i] + 31) >> 5;
+  acc = wave_sum(acc);
+  if (lane == 0) tile_sum[t] = acc;
+}
+
+// exclusive scan of the tile totals in place (one workgroup; ntiles <= 1024 * 8)
+__global__ void __launch_bounds__(1024) k_hf_tile_scan(uint32_t* __restrict__ tile_sum, int ntiles)
+{
+  __shared__ uint32_t s_wave[16];
+  __shared__ uint32_t s_carry;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) s_carry = 0;
+  __syncthreads();
+  for (int base = 0; base < ntiles; base += 1024 * 8) {
+    uint32_t v[8], sum = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int i = base + tid * 8 + k;
+      v[k] = i < ntiles ? tile_sum[i] : 0u;
+      sum += v[k];
+    }
+    const uint32_t inc = wave_incl_scan(sum, lane);
+    if (lane == 63) s_wave[wid] = inc;
+    __syncthreads();
+    uint32_t run = s_carry;
+    for (int w = 0; w < wid; w++) run += s_wave[w];
+    const uint32_t tot = s_carry + [&] { uint32_t t2 = 0; for (int w = 0; w < 16; w++) t2 += s_wave[w]; return t2; }();
+    run += inc - sum;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int i = base + tid * 8 + k;
+      if (i < ntiles) tile_sum[i] = run;
+      run += v[k];
+    }
+    __syncthreads();
+    if (tid == 0) s_carry = tot;
+    __syncthreads();
+  }
+}
+
+// one workgroup per tile: wave 0 turns the tile offset + in-tile exclusive scan into
+// par_entry; then the 4 waves copy the tile's chunks scratch -> bitstream, two chunks per wave
+// per iteration with all their loads issued before the stores.
+__global__ void __launch_bounds__(256) k_hf_gather(HfEncodeArgs a, int cellcap, const uint32_t* __restrict__ tile_off)
+{
+  __shared__ uint32_t s_ent[kGatherTile], s_nc[kGatherTile];
+  const int t = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c0 = t * kGatherTile;
+  if (wid == 0) {
+    const int c = c0 + lane;
+    const uint32_t nc = c < a.pardeg ? (a.par_nbit[c] + 31) >> 5 : 0u;
+    const uint32_t inc = wave_incl_scan(nc, lane);
+    const uint32_t off = tile_off[t] + inc - nc;
+    s_ent[lane] = off, s_nc[lane] = nc;
+    if (c < a.pardeg) a.par_entry[c] = off;
+  }
+  __syncthreads();
+  const int nch = min(kGatherTile, a.pardeg - c0);
+  for (int j = 2 * wid; j < nch; j += 8) {  // chunk pairs (j, j + 1)
+    const int j2 = j + 1;
+    const uint32_t n1 = s_nc[j], e1 = s_ent[j];
+    const uint32_t n2 = j2 < nch ? s_nc[j2] : 0u, e2 = j2 < nch ? s_ent[j2] : 0u;
+    const uint32_t* src1 = a.temp + (size_t)(c0 + j) * cellcap;
+    const uint32_t* src2 = a.temp + (size_t)(c0 + j2) * cellcap;
+    for (uint32_t i = lane; i < max(n1, n2); i += 256) {
+      uint32_t v1[4], v2[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t ii = i + 64 * k;
+        v1[k] = ii < n1 ? src1[ii] : 0u;
+        v2[k] = ii < n2 ? src2[ii] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t ii = i + 64 * k;
+        if (ii < n1) a.bitstream[e1 + ii] = v1[k];
+        if (ii < n2) a.bitstream[e2 + ii] = v2[k];
+      }
+    }
+  }
 }
 
 // ============================== decode ======================================================
@@ -939,8 +1109,39 @@ int hf_encode_groups(int sublen, int pardeg)
   return (pardeg + G - 1) / G;
 }
 
+static size_t hf_encode_tile_words(int pardeg) { return ((size_t)pardeg + kGatherTile - 1) / kGatherTile + 4; }
+
+size_t hf_encode_temp_words(int sublen, int pardeg)
+{  // chunk slots at a worst-case stride, then the per-tile cell totals
+  return enc_wave(sublen) ? (size_t)enc_wave_cellcap(sublen) * (size_t)pardeg + hf_encode_tile_words(pardeg) : 0;
+}
+
 int launch_hf_encode(const HfEncodeArgs& a, hipStream_t st)
 {
+  if (a.temp && enc_wave(a.sublen)) {
+    const int cellcap = enc_wave_cellcap(a.sublen);
+    const size_t lds = (size_t)(((a.bklen + 3) & ~3) + kPackWaves * cellcap) * 4;
+    static int per_cu = 0, ncu = 0;
+    static size_t last_lds = 0;
+    if (lds != last_lds) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_hf_pack, 64 * kPackWaves, lds) != hipSuccess ||
+          per_cu < 1)
+        per_cu = 1;
+      last_lds = lds;
+    }
+    const int need = (a.pardeg + kPackWaves - 1) / kPackWaves;
+    const int grid = need < per_cu * ncu ? need : per_cu * ncu;
+    k_hf_pack<<<grid, 64 * kPackWaves, lds, st>>>(a, cellcap);
+    const int ntiles = (a.pardeg + kGatherTile - 1) / kGatherTile;
+    uint32_t* tile_sum = a.temp + hf_encode_temp_words(a.sublen, a.pardeg) - hf_encode_tile_words(a.pardeg);
+    k_hf_tile_sums<<<(ntiles + 3) / 4, 256, 0, st>>>(a.par_nbit, a.pardeg, tile_sum, ntiles);
+    k_hf_tile_scan<<<1, 1024, 0, st>>>(tile_sum, ntiles);
+    k_hf_gather<<<ntiles, 256, 0, st>>>(a, cellcap, tile_sum);
+    return (int)hipGetLastError();
+  }
   if (enc_wave(a.sublen)) {
     const int cellcap = enc_wave_cellcap(a.sublen);
     const int ngroups = (a.pardeg + kEncW - 1) / kEncW;

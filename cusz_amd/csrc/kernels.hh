@@ -41,8 +41,10 @@ struct HfEncodeArgs {
   uint32_t* bitstream;   // archive segment (4-byte aligned)
   unsigned long long* status;  // pardeg/kGroup+1 lookback words, zeroed before launch
   unsigned int* timeout;       // set nonzero if a bounded spin gave up
+  uint32_t* temp;              // scratch of hf_encode_temp_words(); nullptr = look-back encoder
 };
 int launch_hf_encode(const HfEncodeArgs& a, hipStream_t st);
+size_t hf_encode_temp_words(int sublen, int pardeg);
 
 // decode table scratch (u32 words): L1 4096 | maxl | first[] | bases | L2 2048, then a 32-B
 // sink the lane decoder stores to when it has nothing to flush (HfDecodeArgs::lut)

@@ -33,6 +33,7 @@ namespace cusz_amd {
 
 int build_codebook(const uint32_t* hist, int bklen, uint32_t* book, uint8_t* revbook);
 int hf_encode_groups(int sublen, int pardeg);
+size_t hf_encode_temp_words(int sublen, int pardeg);
 
 int report_hip_error(hipError_t e, const char* expr, const char* file, int line)
 {
@@ -92,6 +93,7 @@ struct Pipeline {
   uint64_t* d_spill = nullptr;
   uint8_t* d_small = nullptr;  // spill_cnt | timeout | info | minmax | extrema scratch
   unsigned long long* d_status = nullptr;
+  uint32_t* d_enc_temp = nullptr;  // encoder scratch (chunk cells at a worst-case stride)
   size_t status_words = 0;
   uint8_t* d_archive = nullptr;
   size_t archive_cap = 0;
@@ -123,13 +125,15 @@ struct Pipeline {
   void release()
   {
     for (void* p : {(void*)d_codes, (void*)d_hist, (void*)d_book, (void*)d_slots, (void*)d_brick_cnt,
-                    (void*)d_brick_off, (void*)d_spill, (void*)d_small, (void*)d_status, (void*)d_archive})
+                    (void*)d_brick_off, (void*)d_spill, (void*)d_small, (void*)d_status, (void*)d_archive,
+                    (void*)d_enc_temp})
       if (p) (void)hipFree(p);
     if (h_xfer) (void)hipHostFree(h_xfer);
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e), e = nullptr;
     d_codes = nullptr, d_hist = nullptr, d_book = nullptr, d_slots = nullptr, d_brick_cnt = nullptr;
     d_brick_off = nullptr, d_spill = nullptr, d_small = nullptr, d_status = nullptr, d_archive = nullptr;
+    d_enc_temp = nullptr;
     h_xfer = nullptr;
   }
 
@@ -174,6 +178,11 @@ struct Pipeline {
   hipError_t alloc_chunk_state()
   {
     if (d_status) (void)hipFree(d_status), d_status = nullptr;
+    if (d_enc_temp) (void)hipFree(d_enc_temp), d_enc_temp = nullptr;
+    if (const size_t tw = hf_encode_temp_words(sublen, pardeg)) {
+      const hipError_t et = hipMalloc(&d_enc_temp, tw * 4);
+      if (et != hipSuccess) return et;
+    }
     if (d_archive) (void)hipFree(d_archive), d_archive = nullptr;
     status_words = (size_t)hf_encode_groups(sublen, pardeg) + 1;
     hipError_t e = hipMalloc(&d_status, status_words * 8);
@@ -287,7 +296,8 @@ struct Pipeline {
                     reinterpret_cast<uint32_t*>(d_archive + phf_off + entry_rel),
                     reinterpret_cast<uint32_t*>(d_archive + phf_off + bits_rel),
                     d_status,
-                    timeout()};
+                    timeout(),
+                    d_enc_temp};
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_hf_encode(ea, stream));
     mark(4);
 
