@@ -534,22 +534,22 @@ __global__ void __launch_bounds__(256) k_hf_gather(HfEncodeArgs a, int cellcap, 
 
 // ============================== decode ======================================================
 // Tables (built once per decompress by k_hf_tables into a device scratch, copied to LDS):
-//  L1: 4096 entries indexed by the next 12 stream bits.  A normal entry resolves one or two
-//      whole codewords: [31:30] nsym (1|2), [29:25] bits of the nsym codes, [24:20] length of
-//      the first code, [19:10] second symbol, [9:0] first symbol.  A prefix that only starts
-//      codes longer than 12 bits holds a pointer: nsym = 0, [29:25] k, [15:0] offset of a
-//      2^k-entry L2 subtable indexed by the k bits after the prefix.
-//  L2: single-symbol entries of the long codes; slot 0 is 0 ("not tabulated").
-// Canonical codes put every long code below first[12] (hf_canon.seq.cc construction: longer
-// codes are numerically smaller), so the pointer prefixes are exactly [0, first[12]) and the
-// longest code under a prefix is the one holding its smallest window value.
+//  L1: 4096 entries indexed by the next 12 stream bits.  An entry resolves one or two whole
+//      codewords: [31:30] nsym (1|2), [29:25] bits of the nsym codes, [24:20] length of the
+//      first code, [19:10] second symbol, [9:0] first symbol; 0 if the code is longer.
+//  L2: single-symbol entries indexed DIRECTLY by the next 16 bits.  Canonical codes put every
+//      code longer than 12 bits below first[12] (hf_canon.seq.cc: longer codes are numerically
+//      smaller), so only windows with a 12-bit prefix < first[12] reach it: the table is
+//      first[12] * 16 entries, and both lookups can be issued together (no pointer chase).
+//  Codes longer than 16 bits (or past the table) take the slow path (threshold counting).
 constexpr int kLutBits = 12;
 constexpr int kL1 = 1 << kLutBits;
 constexpr int kTabMaxl = kL1;       // longest code length
 constexpr int kTabFirst = kL1 + 1;  // [32] first[l] (0 beyond the longest code)
 constexpr int kTabBase = kL1 + 33;  // [32] entry[l] - first[l]
 constexpr int kTabL2 = kL1 + 128;   // second level
-constexpr int kL2Cap = 2048;        // power of two
+constexpr int kL2Cap = 2048;        // second-level entries (the last one stays 0)
+constexpr int kL2Bits = 16;         // second level: codes of up to 16 bits
 static_assert(kTabL2 + kL2Cap <= kHfDecTableWords, "decode table scratch too small");
 constexpr int kLongLens = kLmax - kLutBits;  // lengths only the slow path resolves
 
@@ -587,9 +587,6 @@ __global__ void __launch_bounds__(1024) k_hf_tables(const uint8_t* revbook, int 
 {
   __shared__ uint32_t s_first[32], s_entry[32], s_base[32];
   __shared__ uint16_t s_keys[kMaxBklen];
-  __shared__ uint16_t s_off[kL1];
-  __shared__ uint8_t s_k[kL1];
-  __shared__ uint32_t s_wave[16];
   const int tid = threadIdx.x;
   const int32_t* rv = reinterpret_cast<const int32_t*>(revbook);
   if (tid < 32) s_first[tid] = (uint32_t)rv[tid], s_entry[tid] = (uint32_t)rv[32 + tid];
@@ -598,12 +595,11 @@ __global__ void __launch_bounds__(1024) k_hf_tables(const uint8_t* revbook, int 
   __syncthreads();
   const int maxl = longest_code(s_entry);
   if (tid < 32) {
-    // slow-path copy of first[l] (0xFFFFFFFF past the longest code: never below it)
-    tab[kTabFirst + tid] = (tid >= 1 && tid <= maxl) ? s_first[tid] : 0u;
+    tab[kTabFirst + tid] = (tid >= 1 && tid <= maxl) ? s_first[tid] : 0u;  // slow path
     s_base[tid] = s_entry[tid] - s_first[tid];
     tab[kTabBase + tid] = s_entry[tid] - s_first[tid];
   }
-  if (tid == 0) tab[kTabMaxl] = (uint32_t)maxl, tab[kTabL2] = 0u;
+  if (tid == 0) tab[kTabMaxl] = (uint32_t)maxl;
   __syncthreads();
   uint32_t thr[kLmax + 1];  // first[l]
 #pragma unroll
@@ -611,63 +607,29 @@ __global__ void __launch_bounds__(1024) k_hf_tables(const uint8_t* revbook, int 
   const uint32_t ub = (uint32_t)bklen;
   const uint32_t P = maxl > kLutBits ? min(s_first[kLutBits], (uint32_t)kL1) : 0u;
 
-  // L1 entries (4 prefixes per thread) and the L2 subtable sizes of the pointer prefixes
-  uint32_t e[4], sz[4], tot = 0;
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const uint32_t i = (uint32_t)tid * 4 + j, v = i << (32 - kLutBits);
-    uint32_t s0, s1;
+  // L1: one or two whole codewords of <= 12 bits; 0 for the long-code prefixes [0, P)
+  for (uint32_t i = tid; i < (uint32_t)kL1; i += blockDim.x) {
+    const uint32_t v = i << (32 - kLutBits);
+    uint32_t s0, s1, e = 0;
     const uint32_t l0 = tab_decode1(v, thr, maxl, s_base, s_keys, ub, s0);
-    e[j] = 0, sz[j] = 0;
     if (i >= P && l0 <= (uint32_t)kLutBits) {
       const uint32_t rest = kLutBits - l0;
       const uint32_t l1 = rest ? tab_decode1(v << l0, thr, maxl, s_base, s_keys, ub, s1) : 99u;
-      e[j] = l1 <= rest ? lut_pack(2, l0 + l1, l0, s0, s1) : lut_pack(1, l0, l0, s0, 0);
+      e = l1 <= rest ? lut_pack(2, l0 + l1, l0, s0, s1) : lut_pack(1, l0, l0, s0, 0);
     }
-    else if (i < P && l0 > (uint32_t)kLutBits && l0 <= (uint32_t)kLmax) {
-      sz[j] = 1u << (l0 - kLutBits);  // <= 2^15
-    }
-    tot += sz[j];
+    tab[i] = e;
   }
-  // workgroup exclusive scan of the subtable sizes; offsets start at 1
-  const int lane = tid & 63, wid = tid >> 6;
-  uint32_t inc = tot;
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t t = __shfl_up(inc, d);
-    if (lane >= d) inc += t;
-  }
-  if (lane == 63) s_wave[wid] = inc;
-  __syncthreads();
-  uint32_t off = 1;
-  for (int w = 0; w < wid; w++) off += s_wave[w];
-  off += inc - tot;
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const uint32_t i = (uint32_t)tid * 4 + j;
-    if (sz[j]) {
-      const uint32_t k = 31 - __clz(sz[j]);
-      const bool fits = off + sz[j] <= (uint32_t)kL2Cap;
-      e[j] = fits ? ((k << 25) | off) : 0u;  // 0: slow path
-      s_k[i] = fits ? (uint8_t)k : 0;
-      s_off[i] = (uint16_t)(fits ? off : 0);
-      off += sz[j];
+  // L2 (direct): indexed by the top 16 bits of windows whose 12-bit prefix is < P; codes of
+  // 13..16 bits; 0 (slow path) beyond 16 bits or past the table (its last slot stays 0)
+  const uint32_t n2 = min(P << (kL2Bits - kLutBits), (uint32_t)kL2Cap - 1);
+  for (uint32_t q = tid; q < (uint32_t)kL2Cap; q += blockDim.x) {
+    uint32_t e = 0;
+    if (q < n2) {
+      uint32_t s0;
+      const uint32_t l = tab_decode1(q << (32 - kL2Bits), thr, maxl, s_base, s_keys, ub, s0);
+      if (l <= (uint32_t)kL2Bits) e = lut_pack(1, l, l, s0, 0);
     }
-    else if (i < P) {
-      s_k[i] = 0;  // (inconsistent book) slow path
-    }
-    tab[i] = e[j];
-  }
-  __syncthreads();
-  for (uint32_t p = 0; p < P; p++) {
-    const uint32_t k = s_k[p];
-    if (!k) continue;
-    const uint32_t o = s_off[p];
-    for (uint32_t j = tid; j < (1u << k); j += blockDim.x) {
-      const uint32_t v = (p << (32 - kLutBits)) | (j << (32 - kLutBits - k));
-      uint32_t s;
-      const uint32_t l = tab_decode1(v, thr, maxl, s_base, s_keys, ub, s);
-      tab[kTabL2 + o + j] = lut_pack(1, l, l, s, 0);
-    }
+    tab[kTabL2 + q] = e;
   }
 }
 
@@ -686,16 +648,14 @@ struct HfTables {
   uint32_t first[kLongLens];  // first[l], l = 13..27 (wave-uniform, SGPRs)
 };
 
-// entry for the codeword(s) at the top of `win`: L1, then L2 for long codes (branch-free --
-// with 64 lanes some lane almost always holds a long code), then the rare untabulated case.
+// entry for the codeword(s) at the top of `win`: L1 and L2 read together, then the rare
+// untabulated case
 __device__ __forceinline__ uint32_t hf_entry(const HfTables& t, uint32_t win)
 {
   const uint32_t e1 = t.l1[win >> (32 - kLutBits)];
-  const uint32_t k = (e1 >> 25) & 31u;
-  const uint32_t j = (win << kLutBits) >> 1 >> (31 - k);  // the k bits after the prefix (0 if k = 0)
-  const uint32_t e2 = t.l2[((e1 & 0xFFFFu) + j) & (uint32_t)(kL2Cap - 1)];
+  const uint32_t e2 = t.l2[min(win >> (32 - kL2Bits), (uint32_t)kL2Cap - 1)];
   uint32_t e = (e1 >> 30) ? e1 : e2;
-  if (__builtin_expect(!(e >> 30), 0)) {  // not tabulated: count thresholds (lengths > 12)
+  if (__builtin_expect(!(e >> 30), 0)) {  // count failed lengths (all <= 12 failed)
     uint32_t l = kLutBits + 1;
 #pragma unroll
     for (int q = 0; q < kLongLens; q++) l += (win >> (32 - (kLutBits + 1 + q))) < t.first[q] ? 1u : 0u;
@@ -766,7 +726,7 @@ struct DecProf {
 // a 32-symbol LDS output ring flushed in 32-B stores.  Steps are taken in cadences of kCad
 // (uniform across the wave) so refills and flushes happen at wave-uniform points.
 constexpr int kLpcThreads = 256;
-constexpr int kInStride = 20;   // words per lane: 16 ring cells + 1 mirror + pad (16-B aligned)
+constexpr int kInStride = 20;   // words per lane: 16 ring cells + pad (16-B aligned, staggers banks)
 constexpr int kOutStride = 20;  // words per lane: 32 symbols + pad
 constexpr int kCad = 4;         // <= 4 * 27 bits consumed per cadence < one 128-bit block
 
@@ -821,7 +781,6 @@ __global__ void __launch_bounds__(kLpcThreads) k_hf_decode_lane(HfDecodeArgs a)
   auto ring_put = [&](uint32_t b, uint4 v) {
     if (tail_partial && b == tb_blk) v = tailv;
     reinterpret_cast<uint4*>(ring)[b & 3] = v;
-    if ((b & 3) == 0) ring[16] = v.x;  // mirror: a window starting in cell 15 reads cell 0 as cell 16
   };
 
   // prologue: up to 4 blocks into the ring, two more in flight
@@ -835,8 +794,13 @@ __global__ void __launch_bounds__(kLpcThreads) k_hf_decode_lane(HfDecodeArgs a)
       if ((uint32_t)b < ld) ring_put(b, v[b]);
   }
   uint32_t bA = ld, bB = ld + 1;
-  uint32_t pos = skip * 32, cnt = 0, flushed = 0;
+  uint32_t cnt = 0, flushed = 0;
   uint16_t* gout = a.out + obase;
+  // bit buffer: the next `avail` (>= 32 before every step) stream bits, MSB-aligned; `nxt` is
+  // cell `nw`, read from the ring one refill ahead so the refill never waits on LDS
+  uint64_t buf = ((uint64_t)ring[skip & 15] << 32) | ring[(skip + 1) & 15];
+  uint32_t avail = 64, nw = skip + 2;
+  uint32_t nxt = ring[nw & 15];
 
   // flush 16 symbols (32 B) when a ring half is full (scattered per-lane stores are costly
   // in the address path, so they are issued only when there is something to write)
@@ -853,22 +817,29 @@ __global__ void __launch_bounds__(kLpcThreads) k_hf_decode_lane(HfDecodeArgs a)
   auto steps = [&]() {
 #pragma unroll
     for (int s = 0; s < kCad; s++) {
-      if (cnt < nsym) {
-        const uint32_t* rp = ring + ((pos >> 5) & 15u);
-        const uint32_t win = (uint32_t)((((uint64_t)rp[0] << 32) | rp[1]) >> (32 - (pos & 31u)));
-        const uint32_t e = hf_entry(tb, win);
+      // a lane whose ring has not caught up (never in steady state) skips the step
+      if (cnt < nsym && (nw + 1 < ld * 4 || ld >= nblk)) {
+        const uint32_t e = hf_entry(tb, (uint32_t)(buf >> 32));
         const uint32_t l0 = (e >> 20) & 31u;
         const bool both = (e >> 30) == 2u && cnt + 1 < nsym;
         const uint32_t i0 = cnt & 31u, i1 = both ? ((cnt + 1) & 31u) : i0;
         oring[i0] = (uint16_t)(e & 1023u);
         oring[i1] = (uint16_t)(both ? ((e >> 10) & 1023u) : (e & 1023u));
         cnt += both ? 2u : 1u;
-        pos += both ? ((e >> 25) & 31u) : l0;
+        const uint32_t l = both ? ((e >> 25) & 31u) : l0;
+        buf <<= l;
+        avail -= l;
+        if (avail < 32) {
+          buf |= (uint64_t)nxt << (32 - avail);
+          avail += 32;
+          nw++;
+          nxt = ring[nw & 15];
+        }
       }
     }
   };
   auto cadence = [&](uint4& p, uint32_t& b) {
-    if (b == ld && ld < nblk && ld - (pos >> 7) < 4u) {
+    if (b == ld && ld < nblk && ld - (nw >> 2) < 4u) {
       ring_put(ld, p);
       ld++;
     }

@@ -46,6 +46,8 @@ e = (C.c_ulonglong * (65536 * 4))()
 L.psz_amd_debug_encode_profile(e, 65536 * 4)
 e = np.frombuffer(e, dtype=np.uint64).reshape(65536, 4).astype(np.float64)
 e = e[e.sum(1) > 0]
+if len(e) == 0:
+    sys.exit(0)
 print(f"encoder: {len(e)} workgroups profiled, encode_ms={r.stage_times()[cz.T_ENCODE]:.4f}")
 for k, nm in enumerate(["setup", "pack", "lookback", "write"]):
     print(f"  {nm:8s} cycles/wg: mean={e[:, k].mean():9.0f} p50={np.median(e[:, k]):9.0f} max={e[:, k].max():9.0f}")

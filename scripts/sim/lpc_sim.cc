@@ -68,41 +68,26 @@ int main(int argc, char** argv)
   };
   std::vector<uint32_t> L1(kL1), L2(kL2Cap, 0);
   const uint32_t P = maxl > kLutBits ? std::min(first[kLutBits], (uint32_t)kL1) : 0u;
-  std::vector<uint32_t> sz(kL1, 0);
   for (uint32_t i = 0; i < kL1; i++) {
     uint32_t v = i << 20, s0, s1;
     uint32_t l0 = dec1(v, s0);
+    L1[i] = 0;
     if (i >= P && l0 <= 12) {
       uint32_t rest = 12 - l0;
       uint32_t l1 = rest ? dec1(v << l0, s1) : 99;
       L1[i] = l1 <= rest ? pack(2, l0 + l1, l0, s0, s1) : pack(1, l0, l0, s0, 0);
     }
-    else if (i < P) {
-      assert(l0 > 12 && l0 <= 27);
-      sz[i] = 1u << (l0 - 12);
-    }
+    else if (i < P) assert(l0 > 12 && l0 <= 27);
   }
-  uint32_t off = 1, used = 0;
-  for (uint32_t i = 0; i < P; i++) {
-    uint32_t k = 31 - __builtin_clz(sz[i]);
-    bool fits = off + sz[i] <= (uint32_t)kL2Cap;
-    L1[i] = fits ? ((k << 25) | off) : 0u;
-    if (fits) {
-      for (uint32_t j = 0; j < sz[i]; j++) {
-        uint32_t v = (i << 20) | (j << (20 - k)), s;
-        uint32_t l = dec1(v, s);
-        L2[off + j] = pack(1, l, l, s, 0);
-      }
-      used = off + sz[i];
-    }
-    off += sz[i];
+  const uint32_t n2 = std::min(P << 4, (uint32_t)kL2Cap - 1);
+  for (uint32_t q = 0; q < n2; q++) {
+    uint32_t s0, l = dec1(q << 16, s0);
+    if (l <= 16) L2[q] = pack(1, l, l, s0, 0);
   }
-  printf("maxl=%d P=%u L2 used=%u (wanted %u)\n", maxl, P, used, off);
+  printf("maxl=%d P=%u L2 entries=%u (wanted %u)\n", maxl, P, n2, P << 4);
   auto entry_of = [&](uint32_t win) {
     uint32_t e1 = L1[win >> 20];
-    uint32_t k = (e1 >> 25) & 31u;
-    uint32_t j = (win << 12) >> 1 >> (31 - k);
-    uint32_t e2 = L2[((e1 & 0xFFFFu) + j) & (kL2Cap - 1)];
+    uint32_t e2 = L2[std::min(win >> 16, (uint32_t)kL2Cap - 1)];
     uint32_t e = (e1 >> 30) ? e1 : e2;
     if (!(e >> 30)) {
       uint32_t l = kLutBits + 1;
@@ -162,7 +147,6 @@ int main(int argc, char** argv)
     uint16_t* o16 = (uint16_t*)oring;
     auto ring_put = [&](uint32_t b, const uint32_t v[4]) {
       memcpy(ring + 4 * (b & 3), v, 16);
-      if ((b & 3) == 0) ring[16] = v[0];
     };
     uint32_t ld = std::min(nblk, 4u);
     for (uint32_t b = 0; b < ld; b++) {
@@ -173,31 +157,39 @@ int main(int argc, char** argv)
     uint32_t bA = ld, bB = ld + 1, pA[4], pB[4];
     load_block(bA, pA);
     load_block(bB, pB);
-    uint32_t pos = skip * 32, cnt = 0, flushed = 0;
+    uint32_t cnt = 0, flushed = 0;
+    uint64_t buf = ((uint64_t)ring[skip & 15] << 32) | ring[(skip + 1) & 15];
+    uint32_t avail = 64, nw = skip + 2, nxt = ring[nw & 15];
+    uint64_t consumed = 0;
     auto steps = [&]() {
       for (int s = 0; s < 4; s++) {
         if (cnt < nsym) {
-          // the window's cells must be in the ring
-          uint32_t w = pos >> 5;
-          if (!(w + 1 < ld * 4 || w + 1 >= skip + ncell)) {
-            fprintf(stderr, "chunk %d: ring underrun w=%u ld=%u\n", c, w, ld);
+          if (!(nw + 1 < ld * 4 || ld >= nblk)) {
+            fprintf(stderr, "chunk %d: ring underrun nw=%u ld=%u\n", c, nw, ld);
             exit(3);
           }
-          const uint32_t* rp = ring + (w & 15u);
-          uint32_t win = (uint32_t)((((uint64_t)rp[0] << 32) | rp[1]) >> (32 - (pos & 31u)));
-          uint32_t e = entry_of(win);
+          uint32_t e = entry_of((uint32_t)(buf >> 32));
           uint32_t l0 = (e >> 20) & 31u;
           bool both = (e >> 30) == 2u && cnt + 1 < nsym;
           uint32_t i0 = cnt & 31u, i1 = both ? ((cnt + 1) & 31u) : i0;
           o16[i0] = (uint16_t)(e & 1023u);
           o16[i1] = (uint16_t)(both ? ((e >> 10) & 1023u) : (e & 1023u));
           cnt += both ? 2u : 1u;
-          pos += both ? ((e >> 25) & 31u) : l0;
+          uint32_t l = both ? ((e >> 25) & 31u) : l0;
+          buf <<= l;
+          avail -= l;
+          consumed += l;
+          if (avail < 32) {
+            buf |= (uint64_t)nxt << (32 - avail);
+            avail += 32;
+            nw++;
+            nxt = ring[nw & 15];
+          }
         }
       }
     };
     auto cadence = [&](uint32_t p[4], uint32_t& b) {
-      if (b == ld && ld < nblk && ld - (pos >> 7) < 4u) {
+      if (b == ld && ld < nblk && ld - (nw >> 2) < 4u) {
         ring_put(ld, p);
         ld++;
       }
@@ -217,7 +209,7 @@ int main(int argc, char** argv)
       cadence(pB, bB);
     }
     for (uint32_t i = flushed; i < cnt; i++) out[obase + i] = o16[i & 31u];
-    if ((long long)(pos - skip * 32) != (long long)nbit) max_lag = std::max(max_lag, std::llabs((long long)(pos - skip * 32) - nbit));
+    if ((long long)consumed != (long long)nbit) max_lag = std::max(max_lag, std::llabs((long long)consumed - (long long)nbit));
   }
   FILE* f = fopen((std::string(dir) + "/out.bin").c_str(), "wb");
   fwrite(out.data(), 2, n, f);
