@@ -874,6 +874,204 @@ __global__ void __launch_bounds__(kLpcThreads) k_hf_decode_lane(HfDecodeArgs a)
 #endif
 }
 
+// ---- windowed lane-per-chunk decoder ------------------------------------------------------------
+// Each lane decodes one whole chunk (every codeword decoded once).  The workgroup's 512 chunks
+// are staged through LDS in windows of 16 cells per chunk, double-buffered with LDS-DMA
+// (global_load_lds_dwordx4, four lanes per 64-B window piece, so one DMA instruction fetches
+// 16 chunks' windows as 64-B segments) while the current window is decoded; a barrier separates
+// windows.  Decoding touches only LDS and registers: the bit buffer lives in registers and is
+// refilled from the window one cell ahead; the two table lookups are issued together.  Output
+// goes through a 32-symbol LDS ring per lane and is flushed cooperatively: ready lanes post a
+// request, two helper lanes per request store its 32 B, so stores leave as 32-B segments.
+constexpr int kWinLanes = 512;  // chunks per workgroup (8 waves)
+constexpr int kWin = 16;        // cells per window per chunk
+constexpr int kWinOut = 32;     // output ring symbols per lane
+
+__global__ void __launch_bounds__(kWinLanes) k_hf_decode_win(HfDecodeArgs a)
+{
+  __shared__ __attribute__((aligned(16))) uint32_t s_l1[kL1];
+  __shared__ __attribute__((aligned(16))) uint32_t s_l2[kL2Cap];
+  __shared__ uint32_t s_base[32];
+  __shared__ uint16_t s_keys[kMaxBklen];
+  __shared__ __attribute__((aligned(16))) uint32_t s_in[2 * kWinLanes * kWin];        // [half][lane][16]
+  __shared__ __attribute__((aligned(16))) uint32_t s_out[kWinOut / 2 * kWinLanes];    // [sym pair][lane]
+  __shared__ uint32_t s_gb[kWinLanes];                                                // chunk base, 16-B units
+  __shared__ uint32_t s_lim[kWinLanes];                                               // cells from s_gb (0: none)
+  __shared__ uint32_t s_req[kWinLanes / 64][64];                                      // flush requests per wave
+  __shared__ uint32_t s_nwin;
+  HfTables tb;
+  load_tables(a, s_l1, s_l2, s_base, s_keys, tb);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint32_t c0 = blockIdx.x * kWinLanes;
+  const uint32_t c = c0 + tid;
+  const size_t obase = (size_t)c * a.sublen;
+  const bool live = c < (uint32_t)a.pardeg && obase < a.n;
+  const uint32_t nsym = live ? (uint32_t)min((size_t)a.sublen, a.n - obase) : 0u;
+  const uint32_t nbit = live ? a.par_nbit[c] : 0u;
+  const uint32_t entry = live ? a.par_entry[c] : 0u;
+  const uint32_t ncell = (nbit + 31) >> 5;
+  const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(a.bitstream + entry) & 15);
+  const uint4* gb = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.bitstream + entry) - mis);
+  const uint32_t skip = mis >> 2;
+  const uint32_t lim = live ? skip + ncell : 0u;  // cells of this chunk, counted from gb
+  if (tid == 0) s_nwin = 0;
+  // chunk bases as 16-B offsets from an aligned base (pointers kept in LDS would load as flat)
+  const uint4* gbase = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.bitstream) -
+                                                      (reinterpret_cast<uintptr_t>(a.bitstream) & 15));
+  s_gb[tid] = (uint32_t)(gb - gbase);
+  s_lim[tid] = lim;
+  // the last chunk's final partial 16-B piece is read by cells (never past the stream's end)
+  const bool tail = live && c + 1 == (uint32_t)a.pardeg && (lim & 3);
+  const uint32_t tq = tail ? (lim - 1) & ~3u : 0u;  // first cell of that piece
+  uint32_t t0 = 0, t1 = 0, t2 = 0;
+  if (tail) {
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(gb) + tq;
+    t0 = q[0];
+    if (lim - tq > 1) t1 = q[1];
+    if (lim - tq > 2) t2 = q[2];
+  }
+  __syncthreads();
+  atomicMax(&s_nwin, (lim + kWin - 1) / kWin);
+
+  const uint4* gsafe = reinterpret_cast<const uint4*>(a.lut);
+  // Window w of every chunk is fetched as 32 x (16 chunks x 64 B) segments, four per wave:
+  // lane t covers chunk 16 g + t/4, piece t%4.  Loads go to registers at the start of a
+  // phase and are written to LDS at its end (an LDS-DMA would make every LDS read of the
+  // phase wait for it: the compiler cannot tell the two halves apart).
+  uint4 sv0, sv1, sv2, sv3;
+#define CUSZ_STAGE_LOAD(W)                                                                   \
+  do {                                                                                        \
+    uint4* svp[4] = {&sv0, &sv1, &sv2, &sv3};                                                 \
+    _Pragma("unroll") for (int k = 0; k < 4; k++)                                             \
+    {                                                                                         \
+      const int g = wid * 4 + k;                                                              \
+      const int L = g * 16 + (lane >> 2), j = lane & 3;                                       \
+      const uint32_t q = (W) * kWin + 4 * j;                                                  \
+      const uint32_t ll = s_lim[L];                                                           \
+      const bool tl = (L + c0 + 1 == (uint32_t)a.pardeg) && (ll & 3);                         \
+      const bool ok = q < ll && !(tl && q + 4 > ll);                                          \
+      *svp[k] = *(ok ? gbase + s_gb[L] + (q >> 2) : gsafe);                                   \
+    }                                                                                         \
+  } while (0)
+#define CUSZ_STAGE_STORE(W)                                                                  \
+  do {                                                                                        \
+    uint4* base = reinterpret_cast<uint4*>(s_in + ((W) & 1) * (kWinLanes * kWin) + wid * 64 * kWin); \
+    base[lane] = sv0;                                                                         \
+    base[64 + lane] = sv1;                                                                    \
+    base[128 + lane] = sv2;                                                                   \
+    base[192 + lane] = sv3;                                                                   \
+  } while (0)
+  auto patch_tail = [&](uint32_t w) {  // the owner lane writes its partial piece after the DMA landed
+    if (tail && (tq >> 4) == w) {
+      uint32_t* r = s_in + (w & 1) * (kWinLanes * kWin) + tid * kWin + (tq & 15);
+      r[0] = t0, r[1] = t1, r[2] = t2, r[3] = 0u;
+    }
+  };
+  auto cell = [&](uint32_t n) -> uint32_t { return s_in[((n >> 4) & 1) * (kWinLanes * kWin) + tid * kWin + (n & 15)]; };
+
+  __syncthreads();
+  const uint32_t nwin = s_nwin;
+  CUSZ_STAGE_LOAD(0u);
+  CUSZ_STAGE_STORE(0u);
+  __syncthreads();
+  patch_tail(0);
+
+  uint64_t buf = ((uint64_t)cell(skip) << 32) | cell(skip + 1);
+  uint32_t avail = 64, nw = skip + 2;
+  uint32_t nxt = cell(nw);
+  uint32_t cnt = 0, flushed = 0;
+  // output ring, slot-major ([symbol pair][lane]): a wave's 64 ring writes hit 64 banks
+  uint16_t* oring = reinterpret_cast<uint16_t*>(s_out);
+  auto oslot = [&](uint32_t i) -> uint32_t { return (((i & (kWinOut - 1)) >> 1) * kWinLanes + tid) * 2 + (i & 1); };
+
+  // cooperative flush: ready lanes post (lane << 16 | flushed); helpers store 2 x 16 B each
+  auto flush = [&]() {
+    const bool ready = cnt - flushed >= 16u;
+    const uint64_t m = __ballot(ready);
+    if (!m) return;
+    const uint32_t n = (uint32_t)__popcll(m);
+    if (ready) {
+      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+      s_req[wid][rank] = ((uint32_t)lane << 16) | flushed;
+      flushed += 16;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t i0 = 0; i0 < n; i0 += 32) {
+      const uint32_t i = i0 + (lane >> 1), j = lane & 1;
+      if (i < n) {
+        const uint32_t r = s_req[wid][i];
+        const uint32_t lf = r >> 16, fl = r & 0xFFFFu;
+        const uint32_t L = wid * 64 + lf;
+        const uint32_t* srcw = s_out + (((fl & 16u) >> 1) + 4 * j) * kWinLanes + L;  // 4 symbol pairs
+        const uint4 v = make_uint4(srcw[0], srcw[kWinLanes], srcw[2 * kWinLanes], srcw[3 * kWinLanes]);
+        uint16_t* dst = a.out + (size_t)(c0 + L) * a.sublen + fl + 8 * j;
+        *reinterpret_cast<uint4*>(dst) = v;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  };
+
+  DecProf pf;
+  pf.start();
+  uint32_t iters = 0;
+  for (uint32_t w = 0; w < nwin; w++) {
+    if (w + 1 < nwin) CUSZ_STAGE_LOAD(w + 1);
+    pf.mark(0);
+    const uint32_t wend = (w + 1) * kWin;
+    const bool last_here = lim <= wend;  // all of this chunk's cells are resident
+    while (true) {
+      const bool any = cnt < nsym && (nw + 1 < wend || last_here);
+      if (!__any(any)) break;
+#pragma unroll
+      for (int st = 0; st < kCad; st++) {
+        if (cnt < nsym && (nw + 1 < wend || last_here)) {
+          const uint32_t e = hf_entry(tb, (uint32_t)(buf >> 32));
+          const uint32_t l0 = (e >> 20) & 31u;
+          const bool both = (e >> 30) == 2u && cnt + 1 < nsym;
+          const uint32_t i0 = oslot(cnt), i1 = both ? oslot(cnt + 1) : i0;
+          oring[i0] = (uint16_t)(e & 1023u);
+          oring[i1] = (uint16_t)(both ? ((e >> 10) & 1023u) : (e & 1023u));
+          cnt += both ? 2u : 1u;
+          const uint32_t l = both ? ((e >> 25) & 31u) : l0;
+          buf <<= l;
+          avail -= l;
+          if (avail < 32) {
+            buf |= (uint64_t)nxt << (32 - avail);
+            avail += 32;
+            nw++;
+            nxt = cell(nw);
+          }
+        }
+      }
+      pf.mark(1);
+      if (iters & 1) flush();
+      pf.mark(2);
+      iters++;
+    }
+    if (w + 1 < nwin) CUSZ_STAGE_STORE(w + 1);
+    pf.mark(3);
+    __syncthreads();
+    pf.mark(4);
+    patch_tail(w + 1);
+  }
+  pf.add(8, iters);
+  pf.add(9, nwin);
+  pf.add(13, 1u);
+#ifdef CUSZ_AMD_DEC_PROFILE
+  if (lane == 0 && blockIdx.x * 8 + wid < 4096)
+    for (int q = 0; q < 16; q++) g_dec_prof[(blockIdx.x * 8 + wid) * 16 + q] = pf.v[q];
+#endif
+  // drain: full halves first (cooperatively), then the remainder lane by lane
+  flush();
+  flush();
+  for (uint32_t i = flushed; i < cnt; i++) a.out[obase + i] = oring[oslot(i)];
+#undef CUSZ_STAGE_LOAD
+#undef CUSZ_STAGE_STORE
+}
+
 // ---- wave-per-chunk decoder (for few, long chunks) ------------------------------------------
 constexpr int kDecWaves = 4;   // waves per decode workgroup
 constexpr int kSyncWin = 64;   // bits of a segment whose codeword starts are remembered
@@ -1143,7 +1341,7 @@ int launch_hf_decode(const HfDecodeArgs& a, hipStream_t st)
   // per chunk (three passes, but 64-way parallel inside a chunk).
   const bool lane = a.sublen % 16 == 0 && (a.decoder == 1 || (a.decoder == 0 && a.pardeg >= 64 * ncu));
   if (lane) {
-    k_hf_decode_lane<<<(a.pardeg + kLpcThreads - 1) / kLpcThreads, kLpcThreads, 0, st>>>(a);
+    k_hf_decode_win<<<(a.pardeg + kWinLanes - 1) / kWinLanes, kWinLanes, 0, st>>>(a);
     return (int)hipGetLastError();
   }
   // per wave: staged cells + the chunk's output tile.  The staging area covers the average

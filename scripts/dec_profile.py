@@ -34,12 +34,12 @@ L.psz_amd_debug_decode_profile(buf, 4096 * 16)
 a = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 16).astype(np.float64)
 a = a[a[:, 13] > 0]
 ch = a[:, 13].sum()
-names = ["prologue", "steps", "cadence", "-", "tail"]
+names = ["stage", "steps", "flush", "vmwait", "barrier"]
 tot = a[:, :5].sum()
 print(f"(lane decoder: 'chunks' = waves) waves={len(a)} chunks={int(ch)} chunks/wave={ch/len(a):.1f} decode_ms={r.stage_times()[cz.T_DECODE]:.4f}")
 for k, nm in enumerate(names):
     print(f"  {nm:6s} cycles/chunk={a[:, k].sum()/ch:9.0f}  share={a[:, k].sum()/tot:.3f}")
-print(f"  loop iterations per wave={a[:,8].mean():.1f} (8 steps each)")
+print(f"  loop iterations per wave={a[:,8].mean():.1f} (4 steps each), windows={a[:,9].mean():.1f}")
 print(f"  per-wave total cycles: min={a[:, :5].sum(1).min():.0f} max={a[:, :5].sum(1).max():.0f}")
 
 e = (C.c_ulonglong * (65536 * 4))()
