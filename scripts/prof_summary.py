@@ -30,9 +30,15 @@ for r in rows:
 if len(sys.argv) > 4:
     for d, cname in ((sys.argv[3], "FETCH_SIZE"), (sys.argv[4], "WRITE_SIZE")):
         f = os.path.join(d, "run_counter_collection.csv")
-        shutil.copy(f, os.path.join(out, f"{tag}_pmc_{cname.lower()}.csv"))
+        rows_pmc = list(csv.DictReader(open(f)))
+        keep = [r for r in rows_pmc if "cusz_amd" in r["Kernel_Name"]]
+        if keep:  # only our kernels' rows are kept (the datagen torch kernels are noise)
+            with open(os.path.join(out, f"{tag}_pmc_{cname.lower()}.csv"), "w", newline="") as fo:
+                w = csv.DictWriter(fo, fieldnames=list(keep[0].keys()))
+                w.writeheader()
+                w.writerows(keep)
         acc = {}
-        for r in csv.DictReader(open(f)):
+        for r in rows_pmc:
             if "cusz_amd" not in r["Kernel_Name"] or r["Counter_Name"] != cname:
                 continue
             short = re.search(r"\b(k_\w+)", r["Kernel_Name"]).group(1)
