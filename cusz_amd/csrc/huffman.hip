@@ -1072,6 +1072,210 @@ __global__ void __launch_bounds__(kWinLanes) k_hf_decode_win(HfDecodeArgs a)
 #undef CUSZ_STAGE_STORE
 }
 
+// ---- register-pack lane-per-chunk decoder --------------------------------------------------------
+// One lane per chunk.  The lane keeps the last 8 output symbols in a 4-register shift pack
+// (v_perm_b32 pushes one or two symbols per table step); a two-symbol step never straddles an
+// aligned group of 8 output positions, so the pack completes exactly on group boundaries.  A
+// completed group goes to the lane's 128-B LDS stage with one ds_write_b128; at cadence points a
+// lane whose stage holds a whole 32-symbol block writes it out as 64 contiguous bytes (4 x 16-B
+// stores back to back), so the memory side sees full 64-B segments instead of scattered 16-B
+// pieces (those cost more than the decode itself: measured 630 vs 270 us at 512^3).  The only
+// other LDS traffic of a step is the table lookup and, every ~4 steps, the next input cell from
+// the lane's 16-cell ring.  Partial groups/blocks at unaligned chunk ends use narrower stores.
+constexpr int kPkThreads = 512;
+constexpr int kPkStride = 20;   // input ring words per lane (16 cells, 16-B aligned, banks staggered)
+constexpr int kPkStage = 36;    // stage words per lane (8 groups of 16 B + pad: b128 banks disjoint)
+constexpr uint32_t kSel1 = 0x05040302u;  // v_perm selector: shift the pack by one symbol
+constexpr uint32_t kSel2 = 0x07060504u;  // ... by two symbols
+
+struct Pack8 {
+  uint32_t p0, p1, p2, p3;  // slot j = bits 16(j&1) of p[j>>1]; slot 7 is the newest
+  __device__ __forceinline__ void push(uint32_t s, uint32_t sel)
+  {
+    p0 = __builtin_amdgcn_perm(p1, p0, sel);
+    p1 = __builtin_amdgcn_perm(p2, p1, sel);
+    p2 = __builtin_amdgcn_perm(p3, p2, sel);
+    p3 = __builtin_amdgcn_perm(s, p3, sel);
+  }
+  __device__ __forceinline__ uint16_t slot(int j) const
+  {
+    const uint32_t w = j < 2 ? p0 : j < 4 ? p1 : j < 6 ? p2 : p3;
+    return (uint16_t)(w >> (16 * (j & 1)));
+  }
+};
+
+template <int MODE>  // 0: staged 64-B flushes; 1 (diagnostic): no output; 2 (diagnostic): direct 16-B stores
+__global__ void __launch_bounds__(kPkThreads) k_hf_decode_pk(HfDecodeArgs a)
+{
+  __shared__ __attribute__((aligned(16))) uint32_t s_l1[kL1];
+  __shared__ __attribute__((aligned(16))) uint32_t s_l2[kL2Cap];
+  __shared__ uint32_t s_base[32];
+  __shared__ uint16_t s_keys[kMaxBklen];
+  __shared__ __attribute__((aligned(16))) uint32_t s_in[kPkThreads * kPkStride];
+  __shared__ __attribute__((aligned(16))) uint32_t s_stage[MODE == 0 ? kPkThreads * kPkStage : 4];
+  __shared__ uint32_t s_reqA[kPkThreads / 64][64];
+  __shared__ uint8_t s_reqL[kPkThreads / 64][64];
+  HfTables tb;
+  load_tables(a, s_l1, s_l2, s_base, s_keys, tb);
+
+  const uint32_t c = blockIdx.x * kPkThreads + threadIdx.x;
+  const size_t obase = (size_t)c * a.sublen;
+  const bool live = c < (uint32_t)a.pardeg && obase < a.n;
+  const uint32_t nsym = live ? (uint32_t)min((size_t)a.sublen, a.n - obase) : 0u;
+  const uint32_t nbit = live ? a.par_nbit[c] : 0u;
+  const uint32_t entry = live ? a.par_entry[c] : 0u;
+  const uint32_t ncell = (nbit + 31) >> 5;
+  const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(a.bitstream + entry) & 15);
+  const uint4* gb = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.bitstream + entry) - mis);
+  const uint32_t skip = mis >> 2;
+  const uint32_t nblk = (skip + ncell + 3) >> 2;
+  const bool tail = live && c + 1 == (uint32_t)a.pardeg;
+  const uint4* gsafe = reinterpret_cast<const uint4*>(a.lut);
+  const uint32_t tb_blk = nblk ? nblk - 1 : 0u;
+  const bool tail_partial = tail && nblk && (tb_blk + 1) * 4 > skip + ncell;
+  uint4 tailv = make_uint4(0, 0, 0, 0);
+  if (tail_partial) {
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(gb + tb_blk);
+    const uint32_t lim = skip + ncell - tb_blk * 4;
+    tailv.x = q[0];
+    tailv.y = lim > 1 ? q[1] : 0u;
+    tailv.z = lim > 2 ? q[2] : 0u;
+  }
+  auto load_block = [&](uint32_t b) -> uint4 {
+    const uint32_t bb = min(b, tb_blk);
+    const bool use_tail = tail_partial && bb == tb_blk;
+    return *((live && !use_tail) ? gb + bb : gsafe);
+  };
+  uint32_t* ring = s_in + threadIdx.x * kPkStride;
+  auto ring_put = [&](uint32_t b, uint4 v) {
+    if (tail_partial && b == tb_blk) v = tailv;
+    reinterpret_cast<uint4*>(ring)[b & 3] = v;
+  };
+  uint32_t ld = min(nblk, 4u);
+  {
+    uint4 v[4];
+#pragma unroll
+    for (int b = 0; b < 4; b++) v[b] = load_block(b);
+#pragma unroll
+    for (int b = 0; b < 4; b++)
+      if ((uint32_t)b < ld) ring_put(b, v[b]);
+  }
+  uint32_t bA = ld, bB = ld + 1;
+  uint64_t buf = ((uint64_t)ring[skip & 15] << 32) | ring[(skip + 1) & 15];
+  uint32_t avail = 64, nw = skip + 2;
+  uint32_t nxt = ring[nw & 15];
+
+  // output: absolute index A of the next symbol; groups of 8 are aligned on absolute indices
+  const uint32_t A0 = (uint32_t)obase;
+  const uint32_t Aend = A0 + nsym;
+  const uint32_t Afirst = (A0 + 31) & ~31u;  // first 32-block boundary; earlier groups go direct
+  uint32_t A = A0, Aflushed = Afirst;       // staged blocks flushed up to Aflushed
+  Pack8 pk{0, 0, 0, 0};
+  char* outb = reinterpret_cast<char*>(a.out);
+  uint4* stage = reinterpret_cast<uint4*>(s_stage + (MODE == 0 ? threadIdx.x * kPkStage : 0));
+  auto store_group = [&](uint32_t g0) {  // the pack = positions [g0, g0+8), clipped to [A0, Aend)
+    if (g0 >= A0 && g0 + 8 <= Aend) {
+      *reinterpret_cast<uint4*>(outb + 2 * (size_t)g0) = make_uint4(pk.p0, pk.p1, pk.p2, pk.p3);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const uint32_t pos = g0 + j;
+        if (pos >= A0 && pos < Aend) *reinterpret_cast<uint16_t*>(outb + 2 * (size_t)pos) = pk.slot(j);
+      }
+    }
+  };
+  // Cooperative flush (wave-uniform call): every lane whose stage holds a whole 32-symbol block
+  // posts it; four lanes write each posted block, so a store instruction writes 16 contiguous
+  // 64-B pieces instead of 64 scattered 16-B ones (the address path handles one segment per cycle).
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  auto flush = [&]() {
+    const bool ready = A >= Aflushed + 32;
+    const uint64_t m = __ballot(ready);
+    if (!m) return;
+    // at most 32 blocks per call (two store instructions, so the compiler's vmcnt bookkeeping
+    // stays exact across the loop); a lane produces <= 8 symbols per cadence, so a block waits
+    // at most one extra call and the 8-group stage never wraps onto an unflushed group
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+    if (ready && rank < 32) {
+      s_reqA[wid][rank] = Aflushed;
+      s_reqL[wid][rank] = (uint8_t)lane;
+      Aflushed += 32;
+    }
+    wave_sync();
+    const uint32_t n = min((uint32_t)__popcll(m), 32u);
+#pragma unroll
+    for (uint32_t i0 = 0; i0 < 32; i0 += 16) {
+      const uint32_t i = i0 + (lane >> 2), j = lane & 3;
+      if (i < n) {
+        const uint32_t Af = s_reqA[wid][i];
+        const uint4* st = reinterpret_cast<const uint4*>(s_stage + (wid * 64 + s_reqL[wid][i]) * kPkStage);
+        const uint4 v = st[((Af >> 3) & 4u) + j];
+        *reinterpret_cast<uint4*>(outb + 2 * (size_t)Af + 16 * j) = v;
+      }
+    }
+    wave_sync();
+  };
+
+  auto steps = [&]() {
+#pragma unroll
+    for (int s = 0; s < kCad; s++) {
+      if (A < Aend) {
+        const uint32_t e = hf_entry(tb, (uint32_t)(buf >> 32));
+        const bool both = (e >> 31) && ((A & 7u) != 7u) && (A + 1 < Aend);
+        const uint32_t l = both ? ((e >> 25) & 31u) : ((e >> 20) & 31u);
+        const uint32_t S = (e & 1023u) | ((e << 6) & (1023u << 16));
+        pk.push(S, both ? kSel2 : kSel1);
+        A += both ? 2u : 1u;
+        buf <<= l;
+        avail -= l;
+        if (avail < 32) {
+          buf |= (uint64_t)nxt << (32 - avail);
+          avail += 32;
+          nw++;
+          nxt = ring[nw & 15];
+        }
+        if (MODE != 1 && !(A & 7u)) {
+          if (MODE == 0 && A - 8 >= Afirst)
+            stage[((A - 8) >> 3) & 7u] = make_uint4(pk.p0, pk.p1, pk.p2, pk.p3);
+          else
+            store_group(A - 8);
+        }
+      }
+    }
+  };
+  auto cadence = [&](uint4& p, uint32_t& b) {
+    if (b == ld && ld < nblk && ld - (nw >> 2) < 4u) {
+      ring_put(ld, p);
+      ld++;
+    }
+    if (MODE == 0) flush();
+    if (b < ld) {  // the block went into the ring: fetch the next one of this slot's parity
+      b += 2;
+      p = load_block(b);
+    }
+  };
+  uint4 pA = load_block(bA), pB = load_block(bB);
+  while (__any(A < Aend)) {
+    steps();
+    cadence(pA, bA);
+    steps();
+    cadence(pB, bB);
+  }
+  if (MODE == 0) {
+    while (__any(A >= Aflushed + 32)) flush();
+    // staged groups of an incomplete last block, then the partial last group
+    for (uint32_t g0 = Aflushed; g0 + 8 <= (Aend & ~7u); g0 += 8)
+      *reinterpret_cast<uint4*>(outb + 2 * (size_t)g0) = stage[(g0 >> 3) & 7u];
+  }
+  if (MODE != 1 && live && (Aend & 7u)) {
+    const uint32_t t = Aend & 7u;
+#pragma unroll
+    for (int k = 0; k < 7; k++)
+      if ((uint32_t)k < 8 - t) pk.push(0u, kSel1);
+    store_group(Aend & ~7u);
+  }
+}
+
 // ---- wave-per-chunk decoder (for few, long chunks) ------------------------------------------
 constexpr int kDecWaves = 4;   // waves per decode workgroup
 constexpr int kSyncWin = 64;   // bits of a segment whose codeword starts are remembered
@@ -1339,6 +1543,15 @@ int launch_hf_decode(const HfDecodeArgs& a, hipStream_t st)
   }
   // Many chunks: one lane per chunk (every codeword decoded once).  Few long chunks: one wave
   // per chunk (three passes, but 64-way parallel inside a chunk).
+  if (a.decoder == 4 || a.decoder == 5) {
+    if (a.decoder == 4) k_hf_decode_pk<1><<<(a.pardeg + kPkThreads - 1) / kPkThreads, kPkThreads, 0, st>>>(a);
+    else k_hf_decode_pk<2><<<(a.pardeg + kPkThreads - 1) / kPkThreads, kPkThreads, 0, st>>>(a);
+    return (int)hipGetLastError();
+  }
+  if (a.decoder == 3) {
+    k_hf_decode_pk<0><<<(a.pardeg + kPkThreads - 1) / kPkThreads, kPkThreads, 0, st>>>(a);
+    return (int)hipGetLastError();
+  }
   const bool lane = a.sublen % 16 == 0 && (a.decoder == 1 || (a.decoder == 0 && a.pardeg >= 64 * ncu));
   if (lane) {
     k_hf_decode_win<<<(a.pardeg + kWinLanes - 1) / kWinLanes, kWinLanes, 0, st>>>(a);

@@ -615,7 +615,7 @@ int psz_amd_set_sublen(psz_resource* m, int sublen)
 int psz_amd_set_decoder(psz_resource* m, int kind)
 {
   Pipeline* p = cusz_amd::P(m);
-  if (!p || kind < PSZ_AMD_DECODER_AUTO || kind > PSZ_AMD_DECODER_WAVE) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if (!p || kind < PSZ_AMD_DECODER_AUTO || kind > 8) return PSZ_ABORT_NOT_IMPLEMENTED;
   p->decoder = kind;
   return PSZ_SUCCESS;
 }

@@ -58,11 +58,13 @@ int psz_amd_set_sublen(psz_resource* m, int sublen);
  * segment of a device archive into the manager's code buffer. */
 int psz_amd_decode_codes(psz_resource* m, uint8_t* IN_d_compressed);
 
-/* Huffman decoder selection: 0 auto (default), 1 one lane per chunk, 2 one wave per chunk.
+/* Huffman decoder selection: 0 auto (default), 1 one lane per chunk (LDS-windowed), 2 one wave
+ * per chunk, 3 one lane per chunk (register-pack output).
  * Both decode the same archives bit-exactly; tests exercise both. */
 #define PSZ_AMD_DECODER_AUTO 0
 #define PSZ_AMD_DECODER_LANE 1
 #define PSZ_AMD_DECODER_WAVE 2
+#define PSZ_AMD_DECODER_PACK 3
 int psz_amd_set_decoder(psz_resource* m, int kind);
 
 const char* psz_amd_version(void);

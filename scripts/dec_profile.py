@@ -24,6 +24,9 @@ y = torch.empty_like(x)
 s = torch.cuda.current_stream(dev)
 r = cz.Resource(cz.F4, dims, stream=s.cuda_stream)
 r.enable_timing(True)
+kind = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+if kind:
+    r.set_decoder(kind)
 for _ in range(3):
     ptr, nb, _ = r.compress(x.data_ptr(), eb, cz.Abs)
     r.decompress(ptr, nb, y.data_ptr())
@@ -34,7 +37,10 @@ L.psz_amd_debug_decode_profile(buf, 4096 * 16)
 a = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 16).astype(np.float64)
 a = a[a[:, 13] > 0]
 ch = a[:, 13].sum()
-names = ["stage", "steps", "flush", "vmwait", "barrier"]
+names = ["stage", "steps", "flush", "vmwait", "barrier"] if kind != 2 else ["load", "count", "resync", "emit", "store"]
+if kind == 2:
+    print(f"wave decoder per chunk: max-lane steps count={a[:,8].sum()/ch:.1f} resync={a[:,9].sum()/ch:.1f} "
+          f"emit={a[:,10].sum()/ch:.1f} sync-iterations={a[:,11].sum()/ch:.2f} global-path={a[:,12].sum()/ch:.3f}")
 tot = a[:, :5].sum()
 print(f"(lane decoder: 'chunks' = waves) waves={len(a)} chunks={int(ch)} chunks/wave={ch/len(a):.1f} decode_ms={r.stage_times()[cz.T_DECODE]:.4f}")
 for k, nm in enumerate(names):
