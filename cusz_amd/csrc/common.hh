@@ -29,6 +29,10 @@ struct OutlierSink {
   uint32_t* spill_cnt;   // atomic counter
   uint32_t cap_per_brick;
   uint32_t spill_cap;
+  // nullptr: cells past a brick's slot go to the spill list one by one (order not deterministic).
+  // Otherwise a brick over its slot reserves one contiguous spill range for all of its excess
+  // (spill_start[brick]); the archive then lists every brick's cells in brick order.
+  uint32_t* spill_start = nullptr;
 };
 
 // Device-side summary produced by the finalize kernel and read back by the host once.

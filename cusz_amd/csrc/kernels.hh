@@ -81,6 +81,7 @@ struct FinalizeArgs {
   uint32_t spill_cap;
   uint32_t* brick_off;  // scratch u32[nbricks+1]
   CompressInfo* info;
+  const uint32_t* spill_start = nullptr;  // OutlierSink::spill_start (ranged spill) or nullptr
 };
 int launch_finalize_scan(const FinalizeArgs& a, hipStream_t st);
 
@@ -96,6 +97,7 @@ struct OutlierCopyArgs {
   const CompressInfo* info;
   uint8_t* archive;         // base of the archive
   size_t bitstream_offset;  // byte offset of the bitstream (outliers follow it)
+  const uint32_t* spill_start = nullptr;  // OutlierSink::spill_start (ranged spill) or nullptr
 };
 int launch_outlier_copy(const OutlierCopyArgs& a, hipStream_t st);
 
@@ -113,6 +115,47 @@ struct XferRegions {
 };
 int launch_publish(const XferRegions& r, uint32_t* flag, uint32_t epoch, hipStream_t st);
 int launch_upload(const XferRegions& r, hipStream_t st);
+
+// ---- cuSZ-i spline3 (spline.hip) -----------------------------------------------------------
+struct SplineGeom {
+  uint32_t gdx, gdy, gdz, ntiles;  // 32 x 8 x 8 tiles (spline3.cu:29)
+  size_t anchor_len;               // ceil(x/8) * ceil(y/8) * ceil(z/8) (buf_comp.cc:35-43)
+};
+SplineGeom spline_geom(size_t x, size_t y, size_t z);
+
+template <typename T>
+struct SplineArgs {
+  const T* in;
+  uint32_t X, Y, Z;
+  uint32_t gdx, gdy, gdz, ntiles;
+  float eb_r, ebx2;  // (float)(1/eb), (float)(2 eb): compressor.inl:107-108, FP = float
+  int radius;
+  int bklen;
+  uint16_t* codes;
+  T* anchor;      // anchor_len values (written into the archive's anchor segment)
+  OutlierSink ol; // one slot range per tile (cap_per_brick), spill list beyond
+  uint32_t* hist;
+};
+template <typename T>
+int launch_spline3_c(const SplineArgs<T>& a, hipStream_t st);
+
+template <typename T>
+struct SplineXArgs {
+  const uint16_t* codes;
+  const T* anchor;
+  T* out;
+  uint32_t X, Y, Z;
+  uint32_t gdx, gdy, gdz, ntiles;
+  float eb_r, ebx2;
+  int radius;
+  const uint32_t* boff = nullptr;   // per-tile bucket offsets (set by the launcher)
+  const uint64_t* bucket = nullptr; // outlier cells grouped by tile
+  size_t nbucket = 0;
+};
+// cells: the archive's outlier segment ({f32 code, u32 idx} each); scratch: spline_x_scratch_words
+template <typename T>
+int launch_spline3_x(SplineXArgs<T> a, const uint32_t* cells, size_t ncell, uint32_t* scratch, hipStream_t st);
+size_t spline_x_scratch_words(uint32_t ntiles, size_t ncell);
 
 // min / max (Rel mode, extrema.cuhip.inl:86-208), writes {min, max} as doubles
 template <typename T>

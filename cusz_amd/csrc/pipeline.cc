@@ -77,6 +77,15 @@ struct Pipeline {
   int elem_bytes = 4;
 
   LorenzoGeom geom{};
+  SplineGeom sgeom{};
+  uint32_t spl_cap = 0;           // outlier slots per spline tile
+  size_t spl_slot_cells = 0;      // capacity of the spline slot area (allocated on first use)
+  uint64_t* d_spl_slots = nullptr;
+  uint32_t* d_spl_cnt = nullptr;  // per-tile outlier counts | offsets
+  uint32_t* d_spl_off = nullptr;
+  uint32_t* d_spl_sps = nullptr;  // per-tile spill range starts
+  uint32_t* d_spl_x = nullptr;    // decompression buckets
+  size_t spl_x_words = 0;
   int sublen = 256, pardeg = 1;
   int user_sublen = 0;
   int decoder = 0;  // PSZ_AMD_DECODER_*
@@ -126,7 +135,7 @@ struct Pipeline {
   {
     for (void* p : {(void*)d_codes, (void*)d_hist, (void*)d_book, (void*)d_slots, (void*)d_brick_cnt,
                     (void*)d_brick_off, (void*)d_spill, (void*)d_small, (void*)d_status, (void*)d_archive,
-                    (void*)d_enc_temp})
+                    (void*)d_enc_temp, (void*)d_spl_slots, (void*)d_spl_cnt, (void*)d_spl_off, (void*)d_spl_x, (void*)d_spl_sps})
       if (p) (void)hipFree(p);
     if (h_xfer) (void)hipHostFree(h_xfer);
     for (auto& e : ev)
@@ -134,6 +143,8 @@ struct Pipeline {
     d_codes = nullptr, d_hist = nullptr, d_book = nullptr, d_slots = nullptr, d_brick_cnt = nullptr;
     d_brick_off = nullptr, d_spill = nullptr, d_small = nullptr, d_status = nullptr, d_archive = nullptr;
     d_enc_temp = nullptr;
+    d_spl_slots = nullptr, d_spl_cnt = nullptr, d_spl_off = nullptr, d_spl_x = nullptr, d_spl_sps = nullptr;
+    spl_slot_cells = 0, spl_x_words = 0;
     h_xfer = nullptr;
   }
 
@@ -154,6 +165,8 @@ struct Pipeline {
     CUSZ_AMD_HIP_CHECK(hipGetDevice(&device));
     tune_chunking(n, device, &sublen, &pardeg);
     geom = lorenzo_geom(ndim, l.x, l.y, l.z, elem_bytes);
+    sgeom = spline_geom(l.x, l.y, l.z);
+    spl_cap = (uint32_t)(std::min<size_t>(l.x, 32) * std::min<size_t>(l.y, 8) * std::min<size_t>(l.z, 8) / 10 + 16);
     // outlier capacity: 10 % of the input like the reference (buf_comp.hh:55), as per-brick
     // slots plus an equally large spill list for bricks above 10 %.
     cap_per_brick = geom.brick_elems / 10 + 16;
@@ -187,8 +200,9 @@ struct Pipeline {
     status_words = (size_t)hf_encode_groups(sublen, pardeg) + 1;
     hipError_t e = hipMalloc(&d_status, status_words * 8);
     if (e != hipSuccess) return e;
-    archive_cap = 176 + 128 + rvbk_bytes(kMaxBklen) + 8 * (size_t)pardeg + 4 * bitstream_cells_cap() +
-                  8 * ((size_t)geom.nbricks * cap_per_brick + spill_cap) + 64;
+    const size_t ol_cells = std::max((size_t)geom.nbricks * cap_per_brick, (size_t)sgeom.ntiles * spl_cap);
+    archive_cap = 176 + (size_t)elem_bytes * sgeom.anchor_len + 128 + rvbk_bytes(kMaxBklen) + 8 * (size_t)pardeg +
+                  4 * bitstream_cells_cap() + 8 * (ol_cells + spill_cap) + 64;
     return hipMalloc(&d_archive, archive_cap);
   }
 
@@ -234,9 +248,17 @@ struct Pipeline {
   int compress(psz_header* h, const T* in, uint8_t** out, size_t* outlen)
   {
     const psz_predictor pred = h->pipeline.predictor;
-    if (pred != Lorenzo && pred != LorenzoZigZag) return PSZ_ABORT_NO_SUCH_PREDICTOR;
+    if (pred != Lorenzo && pred != LorenzoZigZag && pred != Spline) return PSZ_ABORT_NO_SUCH_PREDICTOR;
     if (h->pipeline.codec1 != Huffman) return PSZ_ABORT_NO_SUCH_CODEC;
     const bool zz = pred == LorenzoZigZag;
+    const bool spl = pred == Spline;
+    if (spl && !d_spl_slots) {  // spline outlier slots: one range per 32x8x8 tile, allocated on first use
+      spl_slot_cells = (size_t)sgeom.ntiles * spl_cap;
+      CUSZ_AMD_HIP_CHECK(hipMalloc(&d_spl_slots, spl_slot_cells * 8));
+      CUSZ_AMD_HIP_CHECK(hipMalloc(&d_spl_cnt, (size_t)sgeom.ntiles * 4));
+      CUSZ_AMD_HIP_CHECK(hipMalloc(&d_spl_off, ((size_t)sgeom.ntiles + 1) * 4));
+      CUSZ_AMD_HIP_CHECK(hipMalloc(&d_spl_sps, (size_t)sgeom.ntiles * 4));
+    }
     const int radius = h->rc.radius;
     const int bklen = 2 * radius;
     if (radius < 1 || bklen > kMaxBklen) return PSZ_ABORT_NOT_IMPLEMENTED;
@@ -269,16 +291,43 @@ struct Pipeline {
     CUSZ_AMD_HIP_CHECK(hipMemsetAsync(d_status, 0, status_words * 8, stream));
     mark(1);
 
-    OutlierSink ol{d_slots, d_brick_cnt, d_spill, spill_cnt(), cap_per_brick, spill_cap};
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_lorenzo_c<T>(in, len.x, len.y, len.z, eb, radius, zz, geom, d_codes,
-                                                       ol, d_hist, bklen, stream));
+    const size_t anchor_bytes = spl ? sizeof(T) * sgeom.anchor_len : 0;
+    uint64_t* slots = spl ? d_spl_slots : d_slots;
+    uint32_t* bcnt = spl ? d_spl_cnt : d_brick_cnt;
+    uint32_t* boff = spl ? d_spl_off : d_brick_off;
+    const uint32_t nbr = spl ? sgeom.ntiles : geom.nbricks;
+    const uint32_t cap = spl ? spl_cap : cap_per_brick;
+    OutlierSink ol{slots, bcnt, d_spill, spill_cnt(), cap, spill_cap, spl ? d_spl_sps : nullptr};
+    if (spl) {
+      SplineArgs<T> sa{in,
+                       (uint32_t)len.x,
+                       (uint32_t)len.y,
+                       (uint32_t)len.z,
+                       sgeom.gdx,
+                       sgeom.gdy,
+                       sgeom.gdz,
+                       sgeom.ntiles,
+                       (float)(1.0 / eb),
+                       (float)(eb * 2.0),
+                       radius,
+                       bklen,
+                       d_codes,
+                       reinterpret_cast<T*>(d_archive + 176),
+                       ol,
+                       d_hist};
+      CUSZ_AMD_HIP_CHECK((hipError_t)launch_spline3_c<T>(sa, stream));
+    }
+    else {
+      CUSZ_AMD_HIP_CHECK((hipError_t)launch_lorenzo_c<T>(in, len.x, len.y, len.z, eb, radius, zz, geom, d_codes,
+                                                         ol, d_hist, bklen, stream));
+    }
     mark(2);
 
     // codebook on the host (hf_hl.cc:21-34), one round trip
     int fs = fetch(regions({{h_hist(), d_hist, (size_t)bklen * 4}}), 2);
     if (fs) return fs;
     const int rv = build_codebook(h_hist(), bklen, h_book(), h_revbook());
-    const size_t phf_off = 176;  // + anchor bytes (0 for Lorenzo)
+    const size_t phf_off = 176 + anchor_bytes;  // anchors: spline only (compressor.inl:160)
     const size_t rvbk = (size_t)rv;
     const size_t nbit_rel = 128 + rvbk, entry_rel = nbit_rel + 4 * (size_t)pardeg;
     const size_t bits_rel = entry_rel + 4 * (size_t)pardeg;
@@ -301,11 +350,11 @@ struct Pipeline {
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_hf_encode(ea, stream));
     mark(4);
 
-    FinalizeArgs fa{ea.par_nbit, ea.par_entry, pardeg, d_brick_cnt, geom.nbricks, cap_per_brick,
-                    spill_cnt(),  spill_cap,     d_brick_off, info()};
+    FinalizeArgs fa{ea.par_nbit, ea.par_entry, pardeg, bcnt, nbr, cap, spill_cnt(), spill_cap, boff, info(),
+                    ol.spill_start};
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_finalize_scan(fa, stream));
-    OutlierCopyArgs oa{d_slots, d_brick_cnt, d_brick_off, geom.nbricks, cap_per_brick, d_spill,
-                       spill_cnt(), spill_cap, info(), d_archive, phf_off + bits_rel};
+    OutlierCopyArgs oa{slots, bcnt,      boff,           nbr, cap, d_spill, spill_cnt(), spill_cap,
+                       info(), d_archive, phf_off + bits_rel, ol.spill_start};
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_outlier_copy(oa, stream));
 
     // header templates: static fields from the host, dynamic ones filled on the device
@@ -383,9 +432,10 @@ struct Pipeline {
   int decompress(const psz_header* h, const uint8_t* in, T* out)
   {
     const psz_predictor pred = h->pipeline.predictor;
-    if (pred != Lorenzo && pred != LorenzoZigZag) return PSZ_ABORT_NO_SUCH_PREDICTOR;
+    if (pred != Lorenzo && pred != LorenzoZigZag && pred != Spline) return PSZ_ABORT_NO_SUCH_PREDICTOR;
     const bool zz = pred == LorenzoZigZag;
     if (h->len.x != len.x || h->len.y != len.y || h->len.z != len.z) return PSZ_ABORT_UNSUPPORTED_DIMENSION;
+    if (pred == Spline) return decompress_spline<T>(h, in, out);
     mark(6);
     if (zz) CUSZ_AMD_HIP_CHECK(hipMemsetAsync(out, 0, n * sizeof(T), stream));
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_scatter<T>(
@@ -396,6 +446,41 @@ struct Pipeline {
     mark(8);
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_lorenzo_x<T>(d_codes, out, len.x, len.y, len.z, h->rc.eb, h->rc.radius,
                                                        zz, geom, stream));
+    mark(9);
+    return PSZ_SUCCESS;
+  }
+
+  // decode -> (outlier buckets) -> spline reconstruct; the archive's outlier cells hold codes
+  template <typename T>
+  int decompress_spline(const psz_header* h, const uint8_t* in, T* out)
+  {
+    mark(6);
+    const size_t words = spline_x_scratch_words(sgeom.ntiles, h->splen);
+    if (words > spl_x_words) {
+      if (d_spl_x) (void)hipFree(d_spl_x), d_spl_x = nullptr;
+      CUSZ_AMD_HIP_CHECK(hipMalloc(&d_spl_x, words * 4));
+      spl_x_words = words;
+    }
+    mark(7);
+    int s = decode_codes(h, in);
+    if (s) return s;
+    mark(8);
+    const double eb = h->rc.eb;
+    SplineXArgs<T> xa{d_codes,
+                      reinterpret_cast<const T*>(in + h->entry[PSZHEADER_ANCHOR]),
+                      out,
+                      (uint32_t)len.x,
+                      (uint32_t)len.y,
+                      (uint32_t)len.z,
+                      sgeom.gdx,
+                      sgeom.gdy,
+                      sgeom.gdz,
+                      sgeom.ntiles,
+                      (float)(1.0 / eb),
+                      (float)(eb * 2.0),
+                      (int)h->rc.radius};
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_spline3_x<T>(
+        xa, reinterpret_cast<const uint32_t*>(in + h->entry[PSZHEADER_SPFMT]), h->splen, d_spl_x, stream));
     mark(9);
     return PSZ_SUCCESS;
   }

@@ -47,7 +47,7 @@ __global__ void __launch_bounds__(1024) k_finalize_scan(FinalizeArgs a)
 #pragma unroll
     for (int k = 0; k < PER; k++) {
       const uint32_t b = base + tid * PER + k;
-      v[k] = b < a.nbricks ? min(a.brick_cnt[b], a.cap_per_brick) : 0u;
+      v[k] = b < a.nbricks ? (a.spill_start ? a.brick_cnt[b] : min(a.brick_cnt[b], a.cap_per_brick)) : 0u;
       sum += v[k];
     }
     uint32_t inc = sum;
@@ -81,7 +81,7 @@ __global__ void __launch_bounds__(1024) k_finalize_scan(FinalizeArgs a)
     const uint32_t sp_kept = sp < a.spill_cap ? sp : a.spill_cap;
     a.brick_off[a.nbricks] = slot_total;
     a.info->total_ncell = ncell;
-    a.info->splen = (unsigned long long)slot_total + sp_kept;
+    a.info->splen = (unsigned long long)slot_total + (a.spill_start ? 0u : sp_kept);
     a.info->outlier_lost = sp > a.spill_cap ? sp - a.spill_cap : 0u;
   }
 }
@@ -96,7 +96,8 @@ __global__ void __launch_bounds__(256) k_outlier_copy(OutlierCopyArgs a, uint32_
   if (blockIdx.x < brick_blocks) {
     const uint32_t brick = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (brick >= a.nbricks) return;
-    const uint32_t cnt = min(a.brick_cnt[brick], a.cap_per_brick);
+    const uint32_t all = a.brick_cnt[brick];
+    const uint32_t cnt = min(all, a.cap_per_brick);
     const uint64_t* src = a.slots + (size_t)brick * a.cap_per_brick;
     uint32_t* d = dst + 2ull * a.brick_off[brick];
     for (uint32_t i = threadIdx.x & 63; i < cnt; i += 64) {
@@ -104,8 +105,16 @@ __global__ void __launch_bounds__(256) k_outlier_copy(OutlierCopyArgs a, uint32_
       d[2 * i] = (uint32_t)c;
       d[2 * i + 1] = (uint32_t)(c >> 32);
     }
+    if (a.spill_start && all > cnt) {  // this brick's contiguous spill range follows its slot
+      const uint32_t s0 = a.spill_start[brick];
+      for (uint32_t i = threadIdx.x & 63; i < all - cnt; i += 64) {
+        const uint64_t c = s0 + i < a.spill_cap ? a.spill[s0 + i] : 0ull;
+        d[2 * (cnt + i)] = (uint32_t)c;
+        d[2 * (cnt + i) + 1] = (uint32_t)(c >> 32);
+      }
+    }
   }
-  else {
+  else if (!a.spill_start) {
     const uint32_t sp = min(*a.spill_cnt, a.spill_cap);
     uint32_t* d = dst + 2ull * slot_total;
     for (uint32_t i = (blockIdx.x - brick_blocks) * 256 + threadIdx.x; i < sp; i += spill_blocks * 256) {

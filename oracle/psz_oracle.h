@@ -71,6 +71,19 @@ void orc_hf_decode_u2(const uint32_t* bitstream, const uint8_t* revbook, int bkl
                       const uint32_t* par_nbit, const uint32_t* par_entry, int sublen,
                       int pardeg, size_t n, uint16_t* out);
 
+/* cuSZ-i spline3 predictor-quantizer (psz/src/kernel/detail/spline3.inl:916-973, launched by
+ * spline3.cu:22-44) and reconstruction (spline3.inl:975-1016).  PARITY UNPINNED (no reference
+ * test or pipeline exists for this path).  anchors: T[ceil(x/8)*ceil(y/8)*ceil(z/8)];
+ * outliers: (float)code and index, tile order then (z,y,x) inside the tile; returns the count. */
+size_t orc_spline3_c_f32(const float* in, size_t x, size_t y, size_t z, double eb, int radius,
+                         uint16_t* codes, float* anchors, float* ol_val, uint32_t* ol_idx, size_t ol_cap);
+size_t orc_spline3_c_f64(const double* in, size_t x, size_t y, size_t z, double eb, int radius,
+                         uint16_t* codes, double* anchors, float* ol_val, uint32_t* ol_idx, size_t ol_cap);
+void orc_spline3_x_f32(const uint16_t* codes, const float* anchors, const float* ol_val, const uint32_t* ol_idx,
+                       size_t nol, size_t x, size_t y, size_t z, double eb, int radius, float* out);
+void orc_spline3_x_f64(const uint16_t* codes, const double* anchors, const float* ol_val, const uint32_t* ol_idx,
+                       size_t nol, size_t x, size_t y, size_t z, double eb, int radius, double* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -48,6 +48,14 @@ def lib():
             f = getattr(L, name)
             f.restype = None
             f.argtypes = [_P, _P, _P, _SZ, _SZ, _SZ, _SZ, C.c_double, C.c_uint16, C.c_int, _P]
+        for name in ("orc_spline3_c_f32", "orc_spline3_c_f64"):
+            f = getattr(L, name)
+            f.restype = _SZ
+            f.argtypes = [_P, _SZ, _SZ, _SZ, C.c_double, C.c_int, _P, _P, _P, _P, _SZ]
+        for name in ("orc_spline3_x_f32", "orc_spline3_x_f64"):
+            f = getattr(L, name)
+            f.restype = None
+            f.argtypes = [_P, _P, _P, _P, _SZ, _SZ, _SZ, _SZ, C.c_double, C.c_int, _P]
         L.orc_histogram_u2.argtypes = [_P, _SZ, _P, C.c_int]
         L.orc_build_codebook_u2.restype = C.c_int
         L.orc_build_codebook_u2.argtypes = [_P, C.c_int, _P, _P]
@@ -111,6 +119,40 @@ def lorenzo_x(codes, ol_val, ol_idx, dims, eb, radius=512, zigzag=False, dtype=n
     out = np.zeros(n, dtype)
     f = lib().orc_lorenzo_x_f64 if dtype == np.float64 else lib().orc_lorenzo_x_f32
     f(_ptr(codes), _ptr(ol_val), _ptr(ol_idx), len(ol_idx), x, y, z, eb, radius, int(zigzag), _ptr(out))
+    return out
+
+
+def spline_anchor_len(dims):
+    x, y, z = dims
+    return ((x + 7) // 8) * ((y + 7) // 8) * ((z + 7) // 8)
+
+
+def spline3_c(data: np.ndarray, dims, eb: float, radius: int = 512):
+    """cuSZ-i spline3 (parity unpinned) -> (codes u16[N], anchors T[A], ol_val f32[k], ol_idx u32[k]);
+    outliers in tile order, then (z,y,x) inside the 32x8x8 tile."""
+    data = np.ascontiguousarray(data)
+    x, y, z = dims
+    n = x * y * z
+    assert data.size == n and data.dtype in (np.float32, np.float64)
+    codes = np.zeros(n, np.uint16)
+    anchors = np.zeros(spline_anchor_len(dims), data.dtype)
+    ov = np.zeros(max(n, 1), np.float32)
+    oi = np.zeros(max(n, 1), np.uint32)
+    f = lib().orc_spline3_c_f64 if data.dtype == np.float64 else lib().orc_spline3_c_f32
+    k = f(_ptr(data), x, y, z, eb, radius, _ptr(codes), _ptr(anchors), _ptr(ov), _ptr(oi), n)
+    return codes, anchors, ov[:k].copy(), oi[:k].copy()
+
+
+def spline3_x(codes, anchors, ol_val, ol_idx, dims, eb, radius=512):
+    x, y, z = dims
+    n = x * y * z
+    anchors = np.ascontiguousarray(anchors)
+    codes = np.ascontiguousarray(codes, np.uint16)
+    ol_val = np.ascontiguousarray(ol_val, np.float32)
+    ol_idx = np.ascontiguousarray(ol_idx, np.uint32)
+    out = np.zeros(n, anchors.dtype)
+    f = lib().orc_spline3_x_f64 if anchors.dtype == np.float64 else lib().orc_spline3_x_f32
+    f(_ptr(codes), _ptr(anchors), _ptr(ol_val), _ptr(ol_idx), len(ol_idx), x, y, z, eb, radius, _ptr(out))
     return out
 
 

@@ -1,0 +1,116 @@
+"""cuSZ-i spline3 path on the GPU, through the C-ABI, against the CPU oracle.
+
+Parity with the reference itself is UNPINNED (the reference has no test and no wired
+pipeline for spline3, compressor.inl:358-361/:495-497); the oracle restates spline3.inl.
+Bit-exact here: quant codes, anchors, outlier cells (value bits, index AND order: tile order,
+then (z,y,x) inside the 32x8x8 tile), histogram, Huffman segment, and the decompressed field.
+"""
+import numpy as np
+import pytest
+
+import cusz_amd as cz
+from cusz_amd import datagen
+from gpu_util import d2h, empty_device, parse_archive, sync, to_device
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    ((64, 32, 16), np.float32, 1e-3),
+    ((64, 32, 16), np.float64, 1e-3),
+    ((70, 19, 13), np.float32, 3e-6),   # ragged tiles, ~5 % outliers
+    ((70, 19, 13), np.float64, 5e-6),
+    ((45, 37, 1), np.float64, 3e-6),    # 2-D
+    ((1000, 1, 1), np.float32, 3e-6),   # 1-D
+    ((33, 9, 9), np.float32, 3e-6),     # one tile plus its faces
+    ((160, 96, 72), np.float64, 3e-6),
+]
+
+
+def _roundtrip(oracle, dims, dtype, eb, mode=cz.Abs, seed=5):
+    import torch
+
+    n = int(np.prod(dims))
+    data = datagen.smooth3d_np(dims, seed, dtype=dtype)
+    r = cz.Resource(cz.F4 if dtype == np.float32 else cz.F8, dims, cz.Spline)
+    d_in = to_device(data)
+    ptr, nbytes, _ = r.compress(d_in.data_ptr(), eb, mode)
+    arch = d2h(ptr, nbytes).tobytes()
+    a = parse_archive(arch)
+    h = a["header"]
+    assert h.entry[5] == nbytes and h.pipeline.predictor == cz.Spline
+    ebx = h.rc.eb  # absolute (Rel mode scaled by the range)
+    codes_o, anchors_o, ov_o, oi_o = oracle.spline3_c(data, dims, ebx)
+    ino = r.internals()
+    codes_g = d2h(ino.d_quant_codes, 2 * n, np.uint16)
+    bad = np.flatnonzero(codes_g != codes_o)
+    assert bad.size == 0, f"{bad.size} code mismatches, first {bad[:5]}"
+    anchors_g = np.frombuffer(arch[h.entry[1]:h.entry[2]], dtype)
+    np.testing.assert_array_equal(anchors_g.view(np.uint8), anchors_o.view(np.uint8))
+    np.testing.assert_array_equal(a["ol_idx"], oi_o)  # same deterministic order
+    np.testing.assert_array_equal(a["ol_val"].view(np.uint32), ov_o.view(np.uint32))
+    np.testing.assert_array_equal(d2h(ino.d_hist, 4096, np.uint32), oracle.histogram(codes_o))
+    seg_o, _ = oracle.phf_segment(codes_o, 1024, sublen=a["sublen"])
+    assert a["phf"] == seg_o
+    out = empty_device(n, torch.float32 if dtype == np.float32 else torch.float64)
+    out.fill_(float("nan"))
+    r.decompress(ptr, nbytes, out.data_ptr())
+    sync()
+    xg = out.cpu().numpy()
+    xo = oracle.spline3_x(codes_o, anchors_o, ov_o, oi_o, dims, ebx)
+    ub = np.uint32 if dtype == np.float32 else np.uint64
+    bad = np.flatnonzero(xg.view(ub) != xo.view(ub))
+    assert bad.size == 0, f"{bad.size} reconstruction mismatches, first {bad[:5]}"
+    r.close()
+    return data, xg, ebx, len(oi_o)
+
+
+@pytest.mark.parametrize("dims,dtype,eb", CASES)
+def test_spline_parity(oracle, dims, dtype, eb):
+    data, x, ebx, nol = _roundtrip(oracle, dims, dtype, eb)
+    err = np.max(np.abs(x.astype(np.float64) - data))
+    # the reference quantises with float eb parameters (FP = float, spline3.cu:36) and, for f32,
+    # reconstructs in f32: the bound holds up to those roundings
+    tol = 1.001 if dtype == np.float64 else 1.2
+    assert err <= tol * ebx, (err / ebx, nol)
+
+
+def test_spline_too_many_outliers():
+    """More than 10 % outliers -> PSZ_WARN_OUTLIER_TOO_MANY (the reference's cap, buf_comp.hh:55)."""
+    dims = (70, 19, 13)
+    data = datagen.smooth3d_np(dims, 5)
+    r = cz.Resource(cz.F4, dims, cz.Spline)
+    d_in = to_device(data)
+    with pytest.raises(cz.PszError) as e:
+        r.compress(d_in.data_ptr(), 1e-6, cz.Abs)
+    assert e.value.status == cz.PSZ_WARN_OUTLIER_TOO_MANY
+    r.close()
+
+
+def test_spline_rel_mode(oracle):
+    _roundtrip(oracle, (96, 40, 24), np.float64, 1e-6, mode=cz.Rel)
+
+
+def test_spline_fullsize_512(oracle):
+    """BASELINE config 5 size (512^3 f64, r2r 1e-6): error bound and anchors on every element,
+    codes of two tile-aligned slabs against the oracle (tiles are independent)."""
+    import torch
+
+    dims = (512, 512, 512)
+    n = 512 ** 3
+    d_in = datagen.smooth3d_torch(dims, seed=5, device="cuda").double()
+    r = cz.Resource(cz.F8, dims, cz.Spline)
+    ptr, nbytes, _ = r.compress(d_in.data_ptr(), 1e-6, cz.Rel)
+    ebx = r.header.rc.eb
+    out = torch.empty(n, dtype=torch.float64, device="cuda")
+    r.decompress(ptr, nbytes, out.data_ptr())
+    sync()
+    err = (out - d_in).abs().max().item()
+    assert err <= 1.001 * ebx, err / ebx
+    ino = r.internals()
+    codes = d2h(ino.d_quant_codes, 2 * n, np.uint16).reshape(512, 512, 512)
+    host = d_in.cpu().numpy().reshape(512, 512, 512)
+    for z0 in (0, 256):  # slab of 8 planes (+1 face plane for the predictor)
+        sub = np.ascontiguousarray(host[z0:z0 + 9])
+        co, _, _, _ = oracle.spline3_c(sub, (512, 512, 9), ebx)
+        np.testing.assert_array_equal(codes[z0:z0 + 8].ravel(), co.reshape(9, 512, 512)[:8].ravel())
+    r.close()
