@@ -36,8 +36,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--dims", default="512x512x512")
-    ap.add_argument("--eb", type=float, default=1e-4)
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 5],
+                    help="BASELINE.json config: 2 (default, the metric's workload) = 512^3 f32 Lorenzo; "
+                         "1 = CESM-like 3600x1800 f32; 3 = HACC-like 1-D f32 280,953,867; "
+                         "5 = 512^3 f64 cuSZ-i spline, r2r 1e-6")
+    ap.add_argument("--dims", default=None)
+    ap.add_argument("--eb", type=float, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true", help="also time the host-memory (PCIe) path")
     ap.add_argument("--profile-only", action="store_true", help="few steps, no baselines (rocprof)")
@@ -65,15 +69,27 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    dims = tuple(int(v) for v in args.dims.lower().split("x"))
+    cfg = {1: ("3600x1800", 1e-4, cz.Abs, cz.Lorenzo, torch.float32),
+           2: ("512x512x512", 1e-4, cz.Abs, cz.Lorenzo, torch.float32),
+           3: ("280953867", 1e-4, cz.Abs, cz.Lorenzo, torch.float32),
+           5: ("512x512x512", 1e-6, cz.Rel, cz.Spline, torch.float64)}[args.config]
+    dims = tuple(int(v) for v in (args.dims or cfg[0]).lower().split("x"))
     dims = (dims + (1, 1))[:3]
+    args.eb = args.eb if args.eb is not None else cfg[1]
+    mode, predictor, tdt = cfg[2], cfg[3], cfg[4]
+    esz = 8 if tdt == torch.float64 else 4
     n = dims[0] * dims[1] * dims[2]
-    nbytes_in = 4 * n
+    nbytes_in = esz * n
 
-    d_in = datagen.smooth3d_torch(dims, seed=2 + rank, device=dev)
-    d_out = torch.empty(n, dtype=torch.float32, device=dev)
+    if args.config == 1:
+        d_in = torch.from_numpy(datagen.cesm2d_np(dims[:2], seed=1 + rank)).to(dev)
+    elif args.config == 3:
+        d_in = datagen.hacc1d_torch(n, seed=3 + rank, device=dev)
+    else:
+        d_in = datagen.smooth3d_torch(dims, seed=(5 if args.config == 5 else 2) + rank, dtype=tdt, device=dev)
+    d_out = torch.empty(n, dtype=tdt, device=dev)
     stream = torch.cuda.current_stream(dev)
-    r = cz.Resource(cz.F4, dims, stream=stream.cuda_stream)
+    r = cz.Resource(cz.F4 if esz == 4 else cz.F8, dims, predictor, stream=stream.cuda_stream)
     r.enable_timing(True)
 
     def barrier():
@@ -81,7 +97,7 @@ def main():
             tdist.barrier()
 
     def step():
-        ptr, nb, _ = r.compress(d_in.data_ptr(), args.eb, cz.Abs)
+        ptr, nb, _ = r.compress(d_in.data_ptr(), args.eb, mode)
         r.decompress(ptr, nb, d_out.data_ptr())
         return ptr, nb
 
@@ -91,7 +107,11 @@ def main():
 
     # correctness guard on the measured configuration (error bound, every element)
     err = (d_out.double() - d_in.double()).abs().max().item()
-    assert err <= 1.001 * args.eb, f"error bound violated: {err}"
+    eb_abs = r.header.rc.eb  # Rel mode: eb * value range
+    # the reconstruction is computed in T (lrz_x.cuhip.inl / spline3.inl), so T's rounding at the
+    # field's magnitude adds to the bound (f32 at |x| ~ 256, HACC-like config 3: ~8e-6)
+    ulp = (2.0 ** -23 if esz == 4 else 2.0 ** -52) * d_in.abs().max().item()
+    assert err <= 1.001 * eb_abs + ulp, f"error bound violated: {err} > {eb_abs} (+ulp {ulp})"
 
     stage_acc = np.zeros(cz.T_COUNT)
     barrier()
@@ -118,24 +138,34 @@ def main():
     ino = r.internals()
     splen = r.header.splen
     arch_bytes = nb
+    pname = "spline3" if predictor == cz.Spline else "lorenzo"
     kernels = {
-        # predictor: read N*4, write codes N*2 + outlier cells 8/each
-        "lorenzo_c3d": (st[cz.T_PREDICT], 4 * n + 2 * n + 8 * splen),
+        # predictor: read N*esz, write codes N*2 + outlier cells 8/each
+        f"{pname}_c": (st[cz.T_PREDICT], esz * n + 2 * n + 8 * splen),
         # encoder: read codes N*2, write bitstream (archive - metadata)
         "hf_encode": (st[cz.T_ENCODE], 2 * n + arch_bytes),
         # decoder: read bitstream, write codes N*2
         "hf_decode": (st[cz.T_DECODE], arch_bytes + 2 * n),
-        # reconstruct: read codes N*2 (+ sparse outlier plane), write N*4
-        "lorenzo_x3d": (st[cz.T_RECON], 2 * n + 4 * n),
+        # reconstruct: read codes N*2 (+ sparse outlier cells), write N*esz
+        f"{pname}_x": (st[cz.T_RECON], 2 * n + esz * n),
     }
     dom = max(kernels, key=lambda k: kernels[k][0])
     d_ms, d_bytes = kernels[dom]
     achieved = d_bytes / (d_ms * 1e-3) / 1e9 if d_ms > 0 else None
+    # HBM bytes per launch of the same kernel from the committed PMC summary (rocprofv3
+    # FETCH_SIZE/WRITE_SIZE passes of this command, scripts/prof_summary.py); the stage's kernels
+    # by name prefix (the encode stage is k_hf_pack + k_hf_gather)
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    prefixes = {"hf_decode": ["k_hf_decode"], "hf_encode": ["k_hf_pack", "k_hf_gather", "k_hf_encode"],
+                "lorenzo_c": ["k_lorenzo_c"], "lorenzo_x": ["k_lorenzo_x"], "spline3_c": ["k_spline3_c"],
+                "spline3_x": ["k_spline3_x"]}[dom]
     if os.path.exists(pmc_path):
         try:
-            traffic = json.load(open(pmc_path)).get(dom, {}).get("hbm_bytes_per_launch")
+            pmc = json.load(open(pmc_path))
+            hits = [v["hbm_bytes_per_launch"] for k, v in pmc.items()
+                    if any(k.startswith(p) for p in prefixes) and "hbm_bytes_per_launch" in v]
+            traffic = int(sum(hits)) if hits else None
         except Exception:
             traffic = None
     roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1) if achieved else None,
@@ -148,14 +178,14 @@ def main():
     if args.e2e and rank == 0:
         h_in = d_in.cpu().pin_memory()
         h_arch = torch.empty(nb, dtype=torch.uint8).pin_memory()
-        h_out = torch.empty(n, dtype=torch.float32).pin_memory()
+        h_out = torch.empty(n, dtype=tdt).pin_memory()
         d_arch = torch.empty(nb, dtype=torch.uint8, device=dev)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         reps = 3
         for _ in range(reps):
             d_in.copy_(h_in, non_blocking=True)
-            ptr, nb2, _ = r.compress(d_in.data_ptr(), args.eb, cz.Abs)
+            ptr, nb2, _ = r.compress(d_in.data_ptr(), args.eb, mode)
             cz.hip_memcpy(h_arch.data_ptr(), ptr, nb2, 2)
             d_arch[:nb2].copy_(h_arch[:nb2], non_blocking=True)
             r.decompress(d_arch.data_ptr(), nb2, d_out.data_ptr())
@@ -164,12 +194,15 @@ def main():
         e2e = round(nbytes_in * reps / (time.perf_counter() - t1) / 1e9, 2)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_only:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_only and esz == 4 \
+            and predictor == cz.Lorenzo:
         cpu = cpu_baseline(d_in, dims, args.eb, nbytes_in)
 
     if rank == 0:
         line = {
             "metric": "device-resident compress+decompress GB/s (input bytes), 512³ f32 abs eb=1e-4",
+            # configs other than 2 are reported with the same fields for DESIGN.md; only config 2
+            # is the metric's workload
             "value": round(value, 2),
             "unit": "GB/s",
             "n_gpus": world,
@@ -179,10 +212,12 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic (SURVEY.md §8d config-2 field: sin/cos + 1e-3 N(0,1), seed 2+rank)",
-            "config": {"workload": f"config2: {dims[0]}x{dims[1]}x{dims[2]} f32, abs eb={args.eb}, "
-                                   "Lorenzo-3D + histogram + Huffman, compress+decompress per step",
+            "dtype": "f64" if esz == 8 else "f32",
+            "data": f"synthetic (SURVEY.md §8d config-{args.config} recipe, seed per rank)",
+            "config": {"workload": f"config{args.config}: {dims[0]}x{dims[1]}x{dims[2]} "
+                                   f"{'f64' if esz == 8 else 'f32'}, {'rel' if mode == cz.Rel else 'abs'} "
+                                   f"eb={args.eb}, {'spline3' if predictor == cz.Spline else 'Lorenzo'} + "
+                                   "histogram + Huffman, compress+decompress per step",
                        "per_rank_field_bytes": nbytes_in, "parallelism": f"dp{world} (independent fields)"},
             "compress_gbps": round(nbytes_in / (comp_ms * 1e-3) / 1e9, 2) if comp_ms > 0 else None,
             "decompress_gbps": round(nbytes_in / (decomp_ms * 1e-3) / 1e9, 2) if decomp_ms > 0 else None,

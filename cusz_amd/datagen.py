@@ -55,6 +55,20 @@ def smooth3d_torch(dims, seed=2, noise=1e-3, dtype=None, device="cuda"):
     return out
 
 
+def hacc1d_torch(n, seed=3, jump=0.05, device="cuda"):
+    """config 3 on the device (same recipe as hacc1d_np, torch's generator)."""
+    import torch
+
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    steps = torch.randn(n, generator=g, device=device, dtype=torch.float64) * 2e-3
+    jumps = torch.rand(n, generator=g, device=device, dtype=torch.float64) < jump
+    steps = torch.where(jumps, torch.rand(n, generator=g, device=device, dtype=torch.float64) * 256.0, steps)
+    out = torch.remainder(torch.cumsum(steps, 0), 256.0).to(torch.float32)
+    del steps, jumps
+    return out
+
+
 def nyx_fields_torch(dims, seeds=range(10, 16), device="cuda"):
     """config 4: six Nyx-like fields (log-normal density, 3 velocities, temperature)."""
     import torch
