@@ -66,7 +66,8 @@ class psz_header(C.Structure):
 class psz_amd_internals(C.Structure):
     _fields_ = [("d_quant_codes", C.c_void_p), ("d_hist", C.c_void_p), ("d_book", C.c_void_p),
                 ("len", C.c_size_t), ("bklen", C.c_int), ("sublen", C.c_int), ("pardeg", C.c_int),
-                ("ndim", C.c_int), ("splen", C.c_size_t), ("archive_capacity", C.c_size_t)]
+                ("ndim", C.c_int), ("splen", C.c_size_t), ("archive_capacity", C.c_size_t),
+                ("layout", C.c_int), ("brick_width", C.c_int)]
 
 
 assert C.sizeof(psz_header) == 176, C.sizeof(psz_header)
@@ -97,7 +98,7 @@ EXPORTS = [
     "phf_version", "phf_versioninfo",
     # cusz_amd.h
     "psz_amd_get_internals", "psz_amd_enable_timing", "psz_amd_stage_times", "psz_amd_set_sublen",
-    "psz_amd_decode_codes", "psz_amd_set_decoder", "psz_amd_version",
+    "psz_amd_decode_codes", "psz_amd_set_decoder", "psz_amd_set_layout", "psz_amd_version",
 ]
 
 
@@ -138,6 +139,7 @@ def lib():
     L.psz_amd_set_sublen.argtypes = [P, C.c_int]
     L.psz_amd_decode_codes.argtypes = [P, P]
     L.psz_amd_set_decoder.argtypes = [P, C.c_int]
+    L.psz_amd_set_layout.argtypes = [P, C.c_int]
     L.psz_amd_version.restype = C.c_char_p
     L.phf_coarse_tune.argtypes = [C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.pszheader_filesize.restype = C.c_size_t
@@ -148,6 +150,8 @@ def lib():
 
 # Huffman decoder selection (include/cusz_amd.h PSZ_AMD_DECODER_*)
 DECODER_AUTO, DECODER_LANE, DECODER_WAVE = 0, 1, 2
+# archive layout (PSZ_AMD_LAYOUT_*)
+LAYOUT_BRICK, LAYOUT_REFERENCE = 0, 1
 
 
 class PszError(RuntimeError):
@@ -227,6 +231,12 @@ class Resource:
         st = lib().psz_amd_set_decoder(self._h, int(kind))
         if st != PSZ_SUCCESS:
             raise PszError(st, "psz_amd_set_decoder")
+
+    def set_layout(self, layout: int):
+        """LAYOUT_BRICK (fused, default when eligible) or LAYOUT_REFERENCE (byte-identical)."""
+        st = lib().psz_amd_set_layout(self._h, int(layout))
+        if st != PSZ_SUCCESS:
+            raise PszError(st, "psz_amd_set_layout")
 
     def decode_codes(self, d_archive: int):
         st = lib().psz_amd_decode_codes(self._h, C.c_void_p(d_archive))

@@ -1,0 +1,164 @@
+// cusz_amd/csrc/hf_device.hh -- device helpers shared by the Huffman kernels (huffman.hip)
+// and the fused brick kernels (brick.hip): wave64 scans, MSB-first codeword packing into LDS
+// cells, and the canonical-code decode table.
+//
+// Canonical decoding follows the reference rule (codec/hf/src/hf_kernels.cuhip.inl:351-365):
+// the code length is the first l with prefix_l >= first[l]; symbol = keys[entry[l] + prefix_l -
+// first[l]].  revbook layout (hf_bk.seq.cc:135-142): first i32[32] | entry i32[32] | keys[bklen].
+#pragma once
+
+#include "common.hh"
+
+namespace cusz_amd {
+namespace hfd {
+
+// inclusive wave64 prefix sum with DPP (row_shr inside 16-lane rows, then row_bcast15/31)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
+{
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
+{
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d);
+  return v;
+}
+
+__device__ __forceinline__ void wave_sync()
+{
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Pack this lane's codewords (book words: code | len << 27) MSB-first starting at bit `pos`
+// of the LDS cell buffer.  Words only this lane touches are plain stores; the first word (when
+// `pos` is not word aligned) and the trailing partial word may be shared with neighbouring
+// lanes and are merged with LDS atomic OR (the buffer is zero beforehand).
+template <int N>
+__device__ __forceinline__ void pack_words(uint32_t* cells, uint32_t pos, const uint32_t (&w)[N], int mine)
+{
+  uint32_t q = pos >> 5;
+  uint64_t acc = 0;
+  uint32_t fill = pos & 31;
+  bool first = fill != 0;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    if (i >= mine) break;
+    const uint32_t l = w[i] >> 27, v = w[i] & 0x07FFFFFFu;
+    acc |= (uint64_t)v << (64 - fill - l);
+    fill += l;
+    if (fill >= 32) {
+      const uint32_t word = (uint32_t)(acc >> 32);
+      if (first)
+        atomicOr(&cells[q], word);
+      else
+        cells[q] = word;
+      first = false;
+      acc <<= 32;
+      fill -= 32;
+      q++;
+    }
+  }
+  if (fill) atomicOr(&cells[q], (uint32_t)(acc >> 32));
+}
+
+// ---- decode tables --------------------------------------------------------------------------
+// L1 entry for a B-bit window prefix: [31:30] nsym (1|2, 0 = code longer than B bits),
+// [29:25] bits consumed, [24:20] length of the first code, [19:10] second symbol, [9:0] first.
+__device__ __forceinline__ uint32_t lut_pack(uint32_t nsym, uint32_t bits, uint32_t l0, uint32_t s0, uint32_t s1)
+{
+  return (nsym << 30) | (bits << 25) | (l0 << 20) | (s1 << 10) | s0;
+}
+
+// longest code length present (last l with entry[l+1] > entry[l])
+__device__ __forceinline__ int longest_code(const uint32_t* entry)
+{
+  int m = 1;
+  for (int l = 1; l < 31; l++)
+    if (entry[l + 1] > entry[l]) m = l;
+  return m;
+}
+
+// One symbol from a left-justified 32-bit window by the reference rule.  The thresholds
+// first[l] * 2^(32-l) never increase with l (canonical construction), so the failing lengths
+// form a prefix 1..m and the code length is 1 + the number of failing lengths.
+__device__ __forceinline__ uint32_t tab_decode1(uint32_t v, const uint32_t* first, int maxl, const uint32_t* base,
+                                                const uint16_t* keys, uint32_t bklen, uint32_t& sym)
+{
+  uint32_t l = 1;
+#pragma unroll
+  for (int k = 1; k <= kLmax; k++) l += (k <= maxl && (v >> (32 - k)) < first[k]) ? 1u : 0u;
+  if (l > (uint32_t)maxl) l = (uint32_t)maxl;
+  sym = keys[min(base[l] + (v >> (32 - l)), bklen - 1)];
+  return l;
+}
+
+// Decode tables resident in LDS: L1 (2^B entries), keys, base[l] = entry[l] - first[l],
+// first[l] for the slow path (codes longer than B bits).
+template <int B>
+struct LdsTables {
+  uint32_t l1[1 << B];
+  uint32_t first[32];
+  uint32_t base[32];
+  uint32_t entry[32];
+  uint32_t maxl;
+  uint32_t pad[3];
+  uint16_t keys[kMaxBklen];
+};
+
+// Cooperative build by the whole workgroup (ends with a barrier).
+template <int B>
+__device__ __forceinline__ void build_tables(LdsTables<B>& t, const uint8_t* revbook, int bklen)
+{
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int32_t* rv = reinterpret_cast<const int32_t*>(revbook);
+  if (tid < 32) t.first[tid] = (uint32_t)rv[tid], t.entry[tid] = (uint32_t)rv[32 + tid];
+  const uint16_t* keys = reinterpret_cast<const uint16_t*>(revbook + 256);
+  for (int i = tid; i < bklen; i += nt) t.keys[i] = keys[i];
+  __syncthreads();
+  const int maxl = longest_code(t.entry);
+  if (tid < 32) {
+    t.base[tid] = t.entry[tid] - t.first[tid];
+    if (tid == 0) t.maxl = (uint32_t)maxl;
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < (1u << B); i += nt) {
+    const uint32_t v = i << (32 - B);
+    uint32_t s0, s1, e = 0;
+    const uint32_t l0 = tab_decode1(v, t.first, maxl, t.base, t.keys, (uint32_t)bklen, s0);
+    if (l0 <= (uint32_t)B) {
+      const uint32_t rest = B - l0;
+      const uint32_t l1 = rest ? tab_decode1(v << l0, t.first, maxl, t.base, t.keys, (uint32_t)bklen, s1) : 99u;
+      e = l1 <= rest ? lut_pack(2, l0 + l1, l0, s0, s1) : lut_pack(1, l0, l0, s0, 0);
+    }
+    t.l1[i] = e;
+  }
+  __syncthreads();
+}
+
+// Entry for the codeword(s) at the top of `win`; codes longer than B bits are resolved by
+// counting failing lengths (all lengths <= B failed).
+template <int B>
+__device__ __forceinline__ uint32_t lookup(const LdsTables<B>& t, uint32_t win, uint32_t bklen)
+{
+  uint32_t e = t.l1[win >> (32 - B)];
+  if (__builtin_expect(!(e >> 30), 0)) {
+    const uint32_t maxl = t.maxl;
+    uint32_t l = B + 1;
+    for (uint32_t k = B + 1; k < maxl; k++) l += (win >> (32 - k)) < t.first[k] ? 1u : 0u;
+    if (l > maxl) l = maxl;
+    const uint32_t s = t.keys[min(t.base[l] + (win >> (32 - l)), bklen - 1)];
+    e = lut_pack(1, l, l, s, 0);
+  }
+  return e;
+}
+
+}  // namespace hfd
+}  // namespace cusz_amd

@@ -82,6 +82,7 @@ struct FinalizeArgs {
   uint32_t* brick_off;  // scratch u32[nbricks+1]
   CompressInfo* info;
   const uint32_t* spill_start = nullptr;  // OutlierSink::spill_start (ranged spill) or nullptr
+  bool sizes_known = false;  // brick path: total_nbit / total_ncell already in info (reservation)
 };
 int launch_finalize_scan(const FinalizeArgs& a, hipStream_t st);
 
@@ -156,6 +157,45 @@ struct SplineXArgs {
 template <typename T>
 int launch_spline3_x(SplineXArgs<T> a, const uint32_t* cells, size_t ncell, uint32_t* scratch, hipStream_t st);
 size_t spline_x_scratch_words(uint32_t ntiles, size_t ncell);
+
+// ---- fused brick pipeline (brick.hip) --------------------------------------------------------
+// A wave owns a W x 8 x 8 brick (W = 64 V); the Huffman chunk length equals W so each brick row
+// is one chunk.  Eligible: 3-D, lx % W == 0.
+struct BrickGeom {
+  bool ok;
+  int V, W;
+  uint32_t nbx, nby, nbz, nbricks;
+  uint32_t brick_elems;
+  uint32_t nchunks;
+};
+BrickGeom brick_geom(int ndim, size_t lx, size_t ly, size_t lz, int elem_bytes);
+
+struct BrickLaunch {
+  BrickGeom g;
+  uint32_t lx, ly, lz;
+  int grid_scan, grid_pack;  // workgroups of the encode passes (per-device occupancy)
+  int ncu;
+};
+
+// fills ncu and the encode-pass grids for `device`
+int brick_configure(BrickLaunch& L, int elem_bytes, int device);
+
+// LDS bytes of the fused decoder for `waves` waves with `stage_words` staging words each
+size_t brick_decode_lds(uint32_t stage_words, int waves);
+
+template <typename T>
+int launch_brick_scan(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const OutlierSink& ol,
+                      uint32_t* hist, uint16_t* bhist, int bklen, hipStream_t st);
+int launch_brick_reserve(const BrickLaunch& L, const uint16_t* bhist, int bklen, const uint32_t* book, uint32_t* ub,
+                         uint32_t* bbase, CompressInfo* info, hipStream_t st);
+template <typename T>
+int launch_brick_pack(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const uint32_t* book,
+                      int bklen, const uint32_t* bbase, uint32_t* par_nbit, uint32_t* par_entry, uint32_t* bitstream,
+                      int reverse, unsigned int* overflow, hipStream_t st);
+template <typename T>
+int launch_brick_decode(const BrickLaunch& L, const uint32_t* bitstream, const uint8_t* revbook, int bklen,
+                        const uint32_t* par_nbit, const uint32_t* par_entry, T* out, double eb, int radius, bool zz,
+                        uint32_t stage_words, int waves, unsigned int* work, hipStream_t st);
 
 // min / max (Rel mode, extrema.cuhip.inl:86-208), writes {min, max} as doubles
 template <typename T>

@@ -77,6 +77,11 @@ struct Pipeline {
   int elem_bytes = 4;
 
   LorenzoGeom geom{};
+  BrickLaunch bl{};               // fused brick path (brick.hip); bl.g.ok when eligible
+  int layout = 0;                 // PSZ_AMD_LAYOUT_*: 0 brick layout when eligible, 1 reference layout
+  uint16_t* d_bhist = nullptr;    // per-brick u16 histograms (pass 1 -> reservation)
+  uint32_t* d_ub = nullptr;       // per-brick region upper bounds (cells)
+  uint32_t* d_bbase = nullptr;    // exclusive scan of d_ub, nbricks + 1
   SplineGeom sgeom{};
   uint32_t spl_cap = 0;           // outlier slots per spline tile
   size_t spl_slot_cells = 0;      // capacity of the spline slot area (allocated on first use)
@@ -89,6 +94,8 @@ struct Pipeline {
   int sublen = 256, pardeg = 1;
   int user_sublen = 0;
   int decoder = 0;  // PSZ_AMD_DECODER_*
+  int last_layout = 1;   // layout of the last compress (PSZ_AMD_LAYOUT_*)
+  int pack_reverse = 1;  // pass 2 walks bricks last-to-first (reuses pass 1's cache tail)
   uint32_t cap_per_brick = 0, spill_cap = 0;
   size_t splen = 0;
 
@@ -135,7 +142,8 @@ struct Pipeline {
   {
     for (void* p : {(void*)d_codes, (void*)d_hist, (void*)d_book, (void*)d_slots, (void*)d_brick_cnt,
                     (void*)d_brick_off, (void*)d_spill, (void*)d_small, (void*)d_status, (void*)d_archive,
-                    (void*)d_enc_temp, (void*)d_spl_slots, (void*)d_spl_cnt, (void*)d_spl_off, (void*)d_spl_x, (void*)d_spl_sps})
+                    (void*)d_enc_temp, (void*)d_spl_slots, (void*)d_spl_cnt, (void*)d_spl_off, (void*)d_spl_x, (void*)d_spl_sps,
+                    (void*)d_bhist, (void*)d_ub, (void*)d_bbase})
       if (p) (void)hipFree(p);
     if (h_xfer) (void)hipHostFree(h_xfer);
     for (auto& e : ev)
@@ -143,12 +151,22 @@ struct Pipeline {
     d_codes = nullptr, d_hist = nullptr, d_book = nullptr, d_slots = nullptr, d_brick_cnt = nullptr;
     d_brick_off = nullptr, d_spill = nullptr, d_small = nullptr, d_status = nullptr, d_archive = nullptr;
     d_enc_temp = nullptr;
+    d_bhist = nullptr, d_ub = nullptr, d_bbase = nullptr;
     d_spl_slots = nullptr, d_spl_cnt = nullptr, d_spl_off = nullptr, d_spl_x = nullptr, d_spl_sps = nullptr;
     spl_slot_cells = 0, spl_x_words = 0;
     h_xfer = nullptr;
   }
 
   size_t rvbk_bytes(int bklen) const { return 4 * 64 + 2 * (size_t)bklen; }
+  uint32_t brick_cap() const { return bl.g.brick_elems / 10 + 16; }
+  unsigned int* work_counter() { return reinterpret_cast<unsigned int*>(d_small + 32); }
+
+  // fused brick path: 3-D, eligible shape, Lorenzo, default chunking (chunk = brick row)
+  bool use_brick(psz_predictor pred) const
+  {
+    return bl.g.ok && layout == 0 && (pred == Lorenzo || pred == LorenzoZigZag) &&
+           (user_sublen == 0 || user_sublen == bl.g.W);
+  }
 
   size_t bitstream_cells_cap() const { return (n * kLmax + 31) / 32 + (size_t)pardeg + 8; }
 
@@ -171,13 +189,25 @@ struct Pipeline {
     // slots plus an equally large spill list for bricks above 10 %.
     cap_per_brick = geom.brick_elems / 10 + 16;
     spill_cap = (uint32_t)(n / 10 + 1024);
+    bl.g = brick_geom(ndim, l.x, l.y, l.z, elem_bytes);
+    bl.lx = (uint32_t)l.x, bl.ly = (uint32_t)l.y, bl.lz = (uint32_t)l.z;
+    size_t slot_cells = (size_t)geom.nbricks * cap_per_brick;
+    uint32_t max_bricks = geom.nbricks;
+    if (bl.g.ok) {
+      CUSZ_AMD_HIP_CHECK((hipError_t)brick_configure(bl, elem_bytes, device));
+      slot_cells = std::max(slot_cells, (size_t)bl.g.nbricks * brick_cap());
+      max_bricks = std::max(max_bricks, bl.g.nbricks);
+      CUSZ_AMD_HIP_CHECK(hipMalloc(&d_bhist, (size_t)bl.g.nbricks * kMaxBklen * sizeof(uint16_t)));
+      CUSZ_AMD_HIP_CHECK(hipMalloc(&d_ub, (size_t)bl.g.nbricks * 4));
+      CUSZ_AMD_HIP_CHECK(hipMalloc(&d_bbase, ((size_t)bl.g.nbricks + 1) * 4));
+    }
 
     CUSZ_AMD_HIP_CHECK(hipMalloc(&d_codes, (n + 64) * sizeof(uint16_t)));
     CUSZ_AMD_HIP_CHECK(hipMalloc(&d_hist, kMaxBklen * sizeof(uint32_t)));
     CUSZ_AMD_HIP_CHECK(hipMalloc(&d_book, kMaxBklen * sizeof(uint32_t)));
-    CUSZ_AMD_HIP_CHECK(hipMalloc(&d_slots, (size_t)geom.nbricks * cap_per_brick * 8));
-    CUSZ_AMD_HIP_CHECK(hipMalloc(&d_brick_cnt, (size_t)geom.nbricks * 4));
-    CUSZ_AMD_HIP_CHECK(hipMalloc(&d_brick_off, ((size_t)geom.nbricks + 1) * 4));
+    CUSZ_AMD_HIP_CHECK(hipMalloc(&d_slots, slot_cells * 8));
+    CUSZ_AMD_HIP_CHECK(hipMalloc(&d_brick_cnt, (size_t)max_bricks * 4));
+    CUSZ_AMD_HIP_CHECK(hipMalloc(&d_brick_off, ((size_t)max_bricks + 1) * 4));
     CUSZ_AMD_HIP_CHECK(hipMalloc(&d_spill, (size_t)spill_cap * 8));
     CUSZ_AMD_HIP_CHECK(hipMalloc(&d_small, kSmallBytes));
     CUSZ_AMD_HIP_CHECK(hipMemset(d_small, 0, kSmallBytes));
@@ -263,7 +293,8 @@ struct Pipeline {
     const int bklen = 2 * radius;
     if (radius < 1 || bklen > kMaxBklen) return PSZ_ABORT_NOT_IMPLEMENTED;
 
-    if (user_sublen) {
+    const bool brick = use_brick(pred);
+    if (user_sublen && !brick) {
       int s = std::min(8192, ((user_sublen + 255) / 256) * 256);
       if (s != sublen) {
         sublen = s;
@@ -288,8 +319,10 @@ struct Pipeline {
     // per-call state reset (the reference never resets these: SURVEY.md Appendix B.3)
     CUSZ_AMD_HIP_CHECK(hipMemsetAsync(d_hist, 0, (size_t)bklen * 4, stream));
     CUSZ_AMD_HIP_CHECK(hipMemsetAsync(d_small, 0, 64 + sizeof(CompressInfo), stream));
-    CUSZ_AMD_HIP_CHECK(hipMemsetAsync(d_status, 0, status_words * 8, stream));
+    if (!brick) CUSZ_AMD_HIP_CHECK(hipMemsetAsync(d_status, 0, status_words * 8, stream));
     mark(1);
+    last_layout = brick ? PSZ_AMD_LAYOUT_BRICK : PSZ_AMD_LAYOUT_REFERENCE;
+    if (brick) return compress_brick<T>(h, in, out, outlen, eb, radius, zz);
 
     const size_t anchor_bytes = spl ? sizeof(T) * sgeom.anchor_len : 0;
     uint64_t* slots = spl ? d_spl_slots : d_slots;
@@ -370,13 +403,71 @@ struct Pipeline {
     CUSZ_AMD_HIP_CHECK(
         (hipError_t)launch_write_headers(d_archive, h, &ph, info(), phf_off, bits_rel, stream));
     mark(5);
-    fs = fetch(regions({{h_readback(), d_archive, 176},
-                        {h_readback() + 256, info(), sizeof(CompressInfo)},
-                        {h_readback() + 384, timeout(), 4}}),
-               3);
+    return finish_compress(h, out, outlen);
+  }
+
+  // Fused brick compress (brick.hip): pass 1 (histograms + outliers) -> host codebook ->
+  // region reservation -> pass 2 (predict + pack straight into the archive) -> finalize.
+  template <typename T>
+  int compress_brick(psz_header* h, const T* in, uint8_t** out, size_t* outlen, double eb, int radius, bool zz)
+  {
+    const int bklen = 2 * radius;
+    const BrickGeom& g = bl.g;
+    const int bsub = g.W, bpar = (int)g.nchunks;
+    const uint32_t cap = brick_cap();
+    OutlierSink ol{d_slots, d_brick_cnt, d_spill, spill_cnt(), cap, spill_cap, nullptr};
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_scan<T>(bl, in, eb, radius, zz, ol, d_hist, d_bhist, bklen, stream));
+    mark(2);
+
+    int fs = fetch(regions({{h_hist(), d_hist, (size_t)bklen * 4}}), 2);
+    if (fs) return fs;
+    const int rv = build_codebook(h_hist(), bklen, h_book(), h_revbook());
+    const size_t phf_off = 176;
+    const size_t rvbk = (size_t)rv;
+    const size_t nbit_rel = 128 + rvbk, entry_rel = nbit_rel + 4 * (size_t)bpar;
+    const size_t bits_rel = entry_rel + 4 * (size_t)bpar;
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_upload(
+        regions({{d_book, h_book(), (size_t)bklen * 4}, {d_archive + phf_off + 128, h_revbook(), rvbk}}), stream));
+    mark(3);
+
+    uint32_t* par_nbit = reinterpret_cast<uint32_t*>(d_archive + phf_off + nbit_rel);
+    uint32_t* par_entry = reinterpret_cast<uint32_t*>(d_archive + phf_off + entry_rel);
+    uint32_t* bits = reinterpret_cast<uint32_t*>(d_archive + phf_off + bits_rel);
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_reserve(bl, d_bhist, bklen, d_book, d_ub, d_bbase, info(), stream));
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_pack<T>(bl, in, eb, radius, zz, d_book, bklen, d_bbase, par_nbit,
+                                                         par_entry, bits, pack_reverse, timeout(), stream));
+    mark(4);
+
+    FinalizeArgs fa{par_nbit, par_entry, bpar, d_brick_cnt, g.nbricks, cap, spill_cnt(), spill_cap, d_brick_off,
+                    info(), nullptr, true};
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_finalize_scan(fa, stream));
+    OutlierCopyArgs oa{d_slots, d_brick_cnt, d_brick_off, g.nbricks, cap, d_spill, spill_cnt(), spill_cap,
+                       info(), d_archive, phf_off + bits_rel, nullptr};
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_outlier_copy(oa, stream));
+
+    h->vle_sublen = bsub;
+    h->vle_pardeg = bpar;
+    h->len = len;
+    h->entry[0] = 0, h->entry[1] = 176, h->entry[2] = (uint32_t)phf_off;
+    phf_header ph;
+    std::memset(&ph, 0, sizeof(ph));
+    ph.bklen = bklen, ph.sublen = bsub, ph.pardeg = bpar, ph.original_len = n;
+    ph.entry[0] = 0, ph.entry[1] = 128, ph.entry[2] = (uint32_t)nbit_rel, ph.entry[3] = (uint32_t)entry_rel;
+    ph.entry[4] = (uint32_t)bits_rel;
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_write_headers(d_archive, h, &ph, info(), phf_off, bits_rel, stream));
+    mark(5);
+    return finish_compress(h, out, outlen);
+  }
+
+  // read back the device-written header + summary (one flag wait), report status
+  int finish_compress(psz_header* h, uint8_t** out, size_t* outlen)
+  {
+    int fs = fetch(regions({{h_readback(), d_archive, 176},
+                            {h_readback() + 256, info(), sizeof(CompressInfo)},
+                            {h_readback() + 384, timeout(), 4}}),
+                   3);
     if (fs) return fs;
     if (timing) CUSZ_AMD_HIP_CHECK(hipEventSynchronize(ev[5]));
-
     CompressInfo ci;
     std::memcpy(&ci, h_readback() + 256, sizeof(ci));
     unsigned int tmo;
@@ -392,7 +483,7 @@ struct Pipeline {
       stage_ms[PSZ_AMD_T_COMPRESS] = span(0, 5);
     }
     if (tmo) {
-      std::fprintf(stderr, "[cusz_amd] encoder look-back timed out\n");
+      std::fprintf(stderr, "[cusz_amd] encoder reservation/look-back check failed\n");
       return PSZ_ABORT_NOT_IMPLEMENTED;
     }
     if (ci.outlier_lost) return PSZ_WARN_OUTLIER_TOO_MANY;
@@ -441,11 +532,43 @@ struct Pipeline {
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_scatter<T>(
         reinterpret_cast<const uint32_t*>(in + h->entry[PSZHEADER_SPFMT]), h->splen, out, n, stream));
     mark(7);
+    if (bl.g.ok && decoder == 0 && h->vle_sublen == bl.g.W && 2 * h->rc.radius <= kMaxBklen)
+      return decompress_brick<T>(h, in, out, zz);
     int s = decode_codes(h, in);
     if (s) return s;
     mark(8);
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_lorenzo_x<T>(d_codes, out, len.x, len.y, len.z, h->rc.eb, h->rc.radius,
                                                        zz, geom, stream));
+    mark(9);
+    return PSZ_SUCCESS;
+  }
+
+  // fused decode + reconstruct (brick.hip): any archive whose chunk length is the brick width
+  template <typename T>
+  int decompress_brick(const psz_header* h, const uint8_t* in, T* out, bool zz)
+  {
+    const int bklen = 2 * h->rc.radius;
+    const size_t phf_off = h->entry[PSZHEADER_ENCODED];
+    const size_t rvbk = rvbk_bytes(bklen);
+    const int pd = h->vle_pardeg;
+    const uint8_t* phf = in + phf_off;
+    const size_t seg = h->entry[PSZHEADER_ENCODED + 1] - h->entry[PSZHEADER_ENCODED];
+    const size_t fixed = 128 + rvbk + 8 * (size_t)pd;
+    const size_t cells = seg > fixed ? (seg - fixed) / 4 : 0;
+    // LDS staging per wave: the average brick plus margin (bricks above it decode from HBM)
+    const size_t worst = (size_t)bl.g.brick_elems * kLmax / 32 + 64 + 4;
+    size_t stage = cells / std::max<uint32_t>(bl.g.nbricks, 1);
+    stage = std::min(worst, stage + stage / 4 + 96);
+    stage = (stage + 3) / 4 * 4;
+    int waves = 8;
+    while (waves > 1 && brick_decode_lds((uint32_t)stage, waves) > 160 * 1024) waves--;
+    if (brick_decode_lds((uint32_t)stage, waves) > 160 * 1024) stage = 1024;  // tiny stage, HBM reads
+    CUSZ_AMD_HIP_CHECK(hipMemsetAsync(work_counter(), 0, 4, stream));
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_decode<T>(
+        bl, reinterpret_cast<const uint32_t*>(phf + 128 + rvbk + 8 * (size_t)pd), phf + 128, bklen,
+        reinterpret_cast<const uint32_t*>(phf + 128 + rvbk), reinterpret_cast<const uint32_t*>(phf + 128 + rvbk + 4 * (size_t)pd),
+        out, h->rc.eb, h->rc.radius, zz, (uint32_t)stage, waves, work_counter(), stream));
+    mark(8);
     mark(9);
     return PSZ_SUCCESS;
   }
@@ -666,6 +789,8 @@ int psz_amd_get_internals(psz_resource* m, psz_amd_internals* o)
   o->ndim = p->ndim;
   o->splen = p->splen;
   o->archive_capacity = p->archive_cap;
+  o->layout = p->last_layout;
+  o->brick_width = p->bl.g.ok ? p->bl.g.W : 0;
   return PSZ_SUCCESS;
 }
 
@@ -700,8 +825,16 @@ int psz_amd_set_sublen(psz_resource* m, int sublen)
 int psz_amd_set_decoder(psz_resource* m, int kind)
 {
   Pipeline* p = cusz_amd::P(m);
-  if (!p || kind < PSZ_AMD_DECODER_AUTO || kind > 8) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if (!p || kind < PSZ_AMD_DECODER_AUTO || kind > PSZ_AMD_DECODER_WAVE) return PSZ_ABORT_NOT_IMPLEMENTED;
   p->decoder = kind;
+  return PSZ_SUCCESS;
+}
+
+int psz_amd_set_layout(psz_resource* m, int layout)
+{
+  Pipeline* p = cusz_amd::P(m);
+  if (!p || (layout != PSZ_AMD_LAYOUT_BRICK && layout != PSZ_AMD_LAYOUT_REFERENCE)) return PSZ_ABORT_NOT_IMPLEMENTED;
+  p->layout = layout;
   return PSZ_SUCCESS;
 }
 

@@ -75,7 +75,8 @@ __global__ void __launch_bounds__(1024) k_finalize_scan(FinalizeArgs a)
   if (tid == 0) {
     const int last = a.pardeg - 1;
     const unsigned long long ncell =
-        last >= 0 ? (unsigned long long)a.par_entry[last] + ((a.par_nbit[last] + 31u) >> 5) : 0ull;
+        a.sizes_known ? a.info->total_ncell
+                      : (last >= 0 ? (unsigned long long)a.par_entry[last] + ((a.par_nbit[last] + 31u) >> 5) : 0ull);
     const uint32_t slot_total = s_carry;
     const uint32_t sp = *a.spill_cnt;
     const uint32_t sp_kept = sp < a.spill_cap ? sp : a.spill_cap;
@@ -225,7 +226,7 @@ int launch_finalize_scan(const FinalizeArgs& a, hipStream_t st)
 {
   int grid = (a.pardeg + 255) / 256;
   grid = grid < 1 ? 1 : (grid > 128 ? 128 : grid);
-  k_sum_nbit<<<grid, 256, 0, st>>>(a.par_nbit, a.pardeg, &a.info->total_nbit);
+  if (!a.sizes_known) k_sum_nbit<<<grid, 256, 0, st>>>(a.par_nbit, a.pardeg, &a.info->total_nbit);
   k_finalize_scan<<<1, 1024, 0, st>>>(a);
   return (int)hipGetLastError();
 }

@@ -43,6 +43,8 @@ typedef struct psz_amd_internals {
   int ndim;
   size_t splen;            /* outlier cells of the last compress                  */
   size_t archive_capacity; /* bytes reserved for the device archive               */
+  int layout;              /* archive layout of the last compress: PSZ_AMD_LAYOUT_* */
+  int brick_width;         /* chunk length of the brick layout (0: not eligible)  */
 } psz_amd_internals;
 
 int psz_amd_get_internals(psz_resource* m, psz_amd_internals* out);
@@ -58,14 +60,24 @@ int psz_amd_set_sublen(psz_resource* m, int sublen);
  * segment of a device archive into the manager's code buffer. */
 int psz_amd_decode_codes(psz_resource* m, uint8_t* IN_d_compressed);
 
-/* Huffman decoder selection: 0 auto (default), 1 one lane per chunk (LDS-windowed), 2 one wave
- * per chunk, 3 one lane per chunk (register-pack output).
- * Both decode the same archives bit-exactly; tests exercise both. */
+/* Huffman decoder selection: 0 auto (default: the fused brick decoder when the archive's chunk
+ * length is the brick width, else lane/wave by chunk count), 1 one lane per chunk
+ * (LDS-windowed), 2 one wave per chunk.  1 and 2 decode into the code buffer and reconstruct
+ * separately.  All decode the same archives bit-exactly; tests exercise each.  Other values
+ * are rejected. */
 #define PSZ_AMD_DECODER_AUTO 0
 #define PSZ_AMD_DECODER_LANE 1
 #define PSZ_AMD_DECODER_WAVE 2
-#define PSZ_AMD_DECODER_PACK 3
 int psz_amd_set_decoder(psz_resource* m, int kind);
+
+/* Archive layout.  Both are the reference phf format (chunk c of sublen codes at par_entry[c]).
+ *  BRICK (default when eligible: 3-D, x extent a multiple of the brick width): chunk = one brick
+ *    row, predictor fused with the encoder and decoder with the reconstructor; chunks are laid
+ *    out brick by brick with zero cells between brick regions.
+ *  REFERENCE: chunks in index order, no gaps (byte-identical to the reference encoder). */
+#define PSZ_AMD_LAYOUT_BRICK 0
+#define PSZ_AMD_LAYOUT_REFERENCE 1
+int psz_amd_set_layout(psz_resource* m, int layout);
 
 const char* psz_amd_version(void);
 

@@ -66,3 +66,34 @@ def parse_archive(arch: bytes, bklen=1024):
                 total_nbit=tnbit, total_ncell=tncell, phf_entry=pent, revbook=rvbk, par_nbit=par_nbit,
                 par_entry=par_entry, bitstream=bitstream, ol_val=cells[:, 0].view(np.float32).copy(),
                 ol_idx=cells[:, 1].copy())
+
+
+def chunk_cells(par_nbit, par_entry, bitstream):
+    """Concatenate every chunk's cells in chunk order (chunk c: ceil(nbit/32) cells at par_entry[c]),
+    so archives with different chunk placement compare cell for cell.  Also returns the mask of
+    bitstream cells no chunk covers (the brick layout's gaps)."""
+    nc = ((par_nbit.astype(np.int64) + 31) >> 5)
+    starts = par_entry.astype(np.int64)
+    tot = int(nc.sum())
+    idx = np.repeat(starts - np.concatenate(([0], np.cumsum(nc)[:-1])), nc) + np.arange(tot)
+    covered = np.zeros(bitstream.size, bool)
+    covered[idx] = True
+    return bitstream[idx], ~covered
+
+
+def check_phf_against_oracle(a, info, seg_o, layout):
+    """Huffman segment parity.  Reference layout: byte-identical.  Brick layout: identical
+    revbook and par_nbit, every chunk's cells identical, the gaps between brick regions zero."""
+    np.testing.assert_array_equal(a["revbook"], info["revbook"])
+    np.testing.assert_array_equal(a["par_nbit"], info["par_nbit"])
+    if layout == 1:
+        np.testing.assert_array_equal(a["par_entry"], info["par_entry"])
+        np.testing.assert_array_equal(a["bitstream"], info["bitstream"])
+        assert a["phf"] == seg_o, "phf segment bytes differ"
+        return
+    ours, gaps = chunk_cells(a["par_nbit"], a["par_entry"], a["bitstream"])
+    ref, _ = chunk_cells(info["par_nbit"], info["par_entry"], info["bitstream"])
+    np.testing.assert_array_equal(ours, ref)
+    assert not np.any(a["bitstream"][gaps]), "nonzero cells between brick regions"
+    assert a["total_nbit"] == int(info["par_nbit"].astype(np.int64).sum())
+    assert a["total_ncell"] == a["bitstream"].size

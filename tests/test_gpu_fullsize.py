@@ -23,6 +23,8 @@ def _check_full(oracle, d_in, dims, eb, slabs, dtype=np.float32):
     r = cz.Resource(cz.F4 if dtype == np.float32 else cz.F8, dims)
     ptr, nbytes, _ = r.compress(d_in.data_ptr(), eb)
     ino = r.internals()
+    if ino.layout == cz.LAYOUT_BRICK:  # fused path: the codes exist only inside the archive
+        r.decode_codes(ptr)
     codes_t = torch.empty(n, dtype=torch.int16, device="cuda")
     torch.cuda.synchronize()
     import ctypes as C
