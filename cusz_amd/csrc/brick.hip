@@ -37,27 +37,38 @@ namespace {
 
 constexpr int kBrickWaves = 4;  // waves per workgroup in the encode passes
 constexpr int kDecB = 11;       // decode table index bits
-constexpr int kXB = 64;         // decode x-block (symbols per chunk per step)
-constexpr int kPitch = kXB + 2; // LDS code tile row pitch (u16): 33 words, conflict-free column reads
+constexpr int kXB = 32;         // decode x-block (symbols per chunk per step = columns reconstructed)
+constexpr int kPitch = 40;      // LDS code tile row pitch (u16): rows 4 apart are 16 banks apart
 constexpr int kTileWords = 64 * kPitch / 2;
+constexpr int kWorkShards = 8;
+constexpr uint32_t kRingRows = 32;  // decoder input ring rows (power of two): 8 KB per wave
+constexpr int kMaxRefill = 12;      // ring rows refilled per 32-symbol block (registers)  // decoder work counters, 64 B apart (kBrickWorkWords words)
 
 __device__ __forceinline__ uint32_t readlane(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
 
 // ---- 3D brick prediction ----------------------------------------------------------------
 // One y-step of a brick: d[z][k] = Lorenzo residual at (x0 + k, y0 + y, z0 + z) in the
 // reference's order (z-diff, x-diff inside 8-wide tiles, y-diff), lrz_c.cuhip.inl:341-352.
+// the 8 z-rows of one y-step (issued one step ahead of their use: software prefetch)
 template <typename T, int V>
-__device__ __forceinline__ void predict_ystep(const T* __restrict__ in, size_t plane, uint32_t lx, uint32_t lz,
-                                              uint32_t x0, uint32_t gy, uint32_t z0, int y, T ebx2_r,
-                                              T (&bprev)[8][V], T (&p)[8][V])
+__device__ __forceinline__ void load_ystep(const T* __restrict__ in, size_t plane, uint32_t lx, uint32_t ly,
+                                           uint32_t lz, uint32_t x0, uint32_t gy, uint32_t z0, T (&raw)[8][V])
 {
 #pragma unroll
   for (int z = 0; z < 8; z++) {
-    const bool ok = (z0 + z) < lz;
-    load_row<T, V>(in, (size_t)(z0 + z) * plane + (size_t)gy * lx, x0, lx, ok, p[z]);
-#pragma unroll
-    for (int k = 0; k < V; k++) p[z][k] = dround(p[z][k] * ebx2_r);
+    const bool ok = (z0 + z) < lz && gy < ly;
+    load_row<T, V>(in, (size_t)(z0 + z) * plane + (size_t)gy * lx, x0, lx, ok, raw[z]);
   }
+}
+
+template <typename T, int V>
+__device__ __forceinline__ void predict_ystep(const T (&raw)[8][V], uint32_t x0, int y, T ebx2_r, T (&bprev)[8][V],
+                                              T (&p)[8][V])
+{
+#pragma unroll
+  for (int z = 0; z < 8; z++)
+#pragma unroll
+    for (int k = 0; k < V; k++) p[z][k] = dround(raw[z][k] * ebx2_r);
 #pragma unroll
   for (int z = 7; z > 0; z--)
 #pragma unroll
@@ -90,21 +101,29 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
 {
   extern __shared__ uint32_t smem[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint32_t* s_hist = smem + wid * kMaxBklen;
+  uint32_t* s_wg = smem;                                // workgroup histogram (-> global, once)
+  uint32_t* s_hist = smem + (1 + wid) * kMaxBklen;      // this wave's brick histogram
+  for (int i = threadIdx.x; i < bklen; i += blockDim.x) s_wg[i] = 0;
   for (int i = lane; i < bklen; i += 64) s_hist[i] = 0;
-  hfd::wave_sync();
+  __syncthreads();
   const size_t plane = (size_t)lx * ly;
   const uint32_t nw = gridDim.x * kBrickWaves;
   for (uint32_t brick = blockIdx.x * kBrickWaves + wid; brick < nbricks; brick += nw) {
     const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
     const uint32_t x0 = bx * (64 * V) + lane * V, y0 = by * 8, z0 = bz * 8;
     uint32_t cnt = 0;
-    T bprev[8][V];
+    T bprev[8][V], nxt[8][V];
+    load_ystep<T, V>(in, plane, lx, ly, lz, x0, y0, z0, nxt);
     for (int y = 0; y < 8; y++) {
       const uint32_t gy = y0 + y;
       if (gy >= ly) break;
-      T d[8][V];
-      predict_ystep<T, V>(in, plane, lx, lz, x0, gy, z0, y, ebx2_r, bprev, d);
+      T raw[8][V], d[8][V];
+#pragma unroll
+      for (int z = 0; z < 8; z++)
+#pragma unroll
+        for (int k = 0; k < V; k++) raw[z][k] = nxt[z][k];
+      if (y < 7) load_ystep<T, V>(in, plane, lx, ly, lz, x0, gy + 1, z0, nxt);
+      predict_ystep<T, V>(raw, x0, y, ebx2_r, bprev, d);
 #pragma unroll
       for (int z = 0; z < 8; z++) {
         if (z0 + z >= lz) break;
@@ -129,10 +148,15 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
     for (int i = lane; i < bklen; i += 64) {
       const uint32_t c = s_hist[i];
       bh[i] = (uint16_t)c;
-      if (c) atomicAdd(&g_hist[i], c);
+      if (c) atomicAdd(&s_wg[i], c);
       s_hist[i] = 0;
     }
     hfd::wave_sync();
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < bklen; i += blockDim.x) {
+    const uint32_t c = s_wg[i];
+    if (c) atomicAdd(&g_hist[i], c);
   }
 }
 
@@ -241,12 +265,18 @@ k_brick3_pack(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
     const uint32_t base = bbase[brick], lim = bbase[brick + 1] - base;
     uint32_t* dst = bitstream + base;
     uint32_t off = 0, my_nbit = 0, my_entry = 0;
-    T bprev[8][V];
+    T bprev[8][V], nxt[8][V];
+    load_ystep<T, V>(in, plane, lx, ly, lz, x0, y0, z0, nxt);
     for (int y = 0; y < 8; y++) {
       const uint32_t gy = y0 + y;
       if (gy >= ly) break;
-      T d[8][V];
-      predict_ystep<T, V>(in, plane, lx, lz, x0, gy, z0, y, ebx2_r, bprev, d);
+      T raw[8][V], d[8][V];
+#pragma unroll
+      for (int z = 0; z < 8; z++)
+#pragma unroll
+        for (int k = 0; k < V; k++) raw[z][k] = nxt[z][k];
+      if (y < 7) load_ystep<T, V>(in, plane, lx, ly, lz, x0, gy + 1, z0, nxt);
+      predict_ystep<T, V>(raw, x0, y, ebx2_r, bprev, d);
 #pragma unroll
       for (int z = 0; z < 8; z++) {
         if (z0 + z >= lz) break;
@@ -285,73 +315,129 @@ k_brick3_pack(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
 }
 
 // =========================================================================================
-// decompress: staged chunk decode + reconstruct, one wave per brick
+// decompress: chunk decode + reconstruct, one wave per brick
 // =========================================================================================
+// Input staging.  Lane l decodes chunk l (brick row (y, z) = (l / 8, l % 8)).  The words of all
+// 64 chunks are staged in an LDS ring laid out [word k][lane]: row k holds word k of every chunk,
+// filled by one LDS-DMA instruction with per-lane source addresses (lane-linear destination),
+// so a lane's reads ring[(k % R) * 64 + lane] never conflict.  Rows are issued a block ahead and
+// land while the current block decodes; a lane that outruns the resident rows reads HBM.
 struct BitReader {
-  uint64_t buf;
-  uint32_t avail, nw, nxt;
+  uint64_t buf;    // next bits of the chunk, left-justified
+  uint32_t avail;  // valid bits in buf (>= 32 between steps)
+  uint32_t nw;     // index of the next chunk word to append
 };
 
-// decode up to kXB symbols of this lane's chunk into its row of the code tile.
-// FETCH(k) returns the k-th word of the lane's chunk (zero past its end).
-template <typename Fetch>
-__device__ __forceinline__ void decode_block(const hfd::LdsTables<kDecB>& tb, uint32_t bklen, bool live,
-                                             BitReader& br, int& pend, uint16_t* row, Fetch fetch)
+// LDS pointer type: keeps ring reads ds_read_* (a generic pointer that may alias global memory
+// would become a flat load, which waits on every outstanding DMA and store)
+using lds_u32 = __attribute__((address_space(3))) const uint32_t;
+
+struct Ring {
+  lds_u32* ring;         // this wave's kRingRows x 64 words, row k % kRingRows holds chunk word k
+  uint32_t valid_top;    // rows [.., valid_top) have landed
+  const uint32_t* gsrc;  // this lane's chunk in HBM (fallback past the resident rows)
+  uint32_t nc;           // words in this lane's chunk
+};
+
+// A chunk word the ring does not hold yet, read from HBM.  The load and its wait are inline asm
+// so the compiler's wait insertion does not place a vmcnt(0) -- which would also wait for every
+// in-flight ring DMA and output store -- at the join after this rare branch on the common path.
+__device__ __forceinline__ uint32_t fallback_word(const Ring& rs, uint32_t k)
+{
+  if (k >= rs.nc) return 0u;
+  uint32_t v;
+  asm volatile("global_load_dword %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(rs.gsrc + k) : "memory");
+  return v;
+}
+
+// decode kXB symbols of this lane's chunk into its tile row (plus a carried symbol when a
+// two-symbol step crossed the previous block's end; the row has slack for the overrun).
+// Branch-free step: the L1/L2 entries and the next input word are read together; a finished
+// lane keeps stepping with a zero length (no state change) until the whole wave is done.
+__device__ __forceinline__ void decode_block(const hfd::LdsTables<kDecB>& tb, const hfd::DecRegs& rg, uint32_t bklen,
+                                             bool live, BitReader& br, int& carry, uint16_t* row, const Ring& rs,
+                                             int lane)
 {
   uint32_t cnt = 0;
-  if (live && pend >= 0) row[0] = (uint16_t)pend, cnt = 1, pend = -1;
-  if (!live) cnt = kXB;
+  if (carry >= 0) row[0] = (uint16_t)carry, cnt = 1;
+  carry = -1;
+  if (!live) cnt = kXB + 1;
   while (__builtin_amdgcn_ballot_w64(cnt < kXB)) {
 #pragma unroll
     for (int st = 0; st < 4; st++) {
-      if (cnt < kXB) {
-        const uint32_t e = hfd::lookup<kDecB>(tb, (uint32_t)(br.buf >> 32), bklen);
-        const bool two = (e >> 30) == 2u;
-        row[cnt] = (uint16_t)(e & 1023u);
-        if (two) {
-          const uint16_t s1 = (uint16_t)((e >> 10) & 1023u);
-          if (cnt + 1 < kXB) row[cnt + 1] = s1;
-          else pend = s1;
-        }
-        cnt = min(cnt + (two ? 2u : 1u), (uint32_t)kXB);
-        const uint32_t l = two ? ((e >> 25) & 31u) : ((e >> 20) & 31u);
-        br.buf <<= l;
-        br.avail -= l;
-        if (br.avail < 32) {
-          br.buf |= (uint64_t)br.nxt << (32 - br.avail);
-          br.avail += 32;
-          br.nw++;
-          br.nxt = fetch(br.nw);
-        }
-      }
+      const uint32_t win = (uint32_t)(br.buf >> 32);
+      uint32_t nxt = rs.ring[(br.nw & (kRingRows - 1)) * 64 + lane];
+      if (__builtin_expect(br.nw >= rs.valid_top, 0)) nxt = fallback_word(rs, br.nw);
+      const uint32_t e = hfd::lookup<kDecB>(tb, rg, win, bklen);
+      const bool act = cnt < kXB;
+      const uint32_t c = min(cnt, (uint32_t)kXB + 1);
+      row[c] = (uint16_t)(e & 1023u);
+      row[c + 1] = (uint16_t)((e >> 10) & 1023u);  // overwritten next step unless two symbols
+      const uint32_t l = act ? ((e >> 25) & 31u) : 0u;  // bits consumed (1 or 2 codes)
+      cnt += act ? (e >> 30) : 0u;
+      br.buf <<= l;
+      br.avail -= l;
+      const bool rf = br.avail < 32;
+      br.buf |= rf ? ((uint64_t)nxt << (32 - br.avail)) : 0ull;
+      br.avail += rf ? 32u : 0u;
+      br.nw += rf ? 1u : 0u;
     }
   }
+  if (cnt == kXB + 1 && live) carry = row[kXB];
 }
 
+__device__ __forceinline__ uint32_t wave_min(uint32_t v)
+{
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v = min(v, (uint32_t)__shfl_xor(v, d));
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t v)
+{
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d));
+  return v;
+}
+
+constexpr int kDecMaxWaves = 12;  // 3 waves per SIMD: up to 168 VGPRs without spills
+
 template <typename T, int V, bool ZZ>
-__global__ void __launch_bounds__(512)
+__global__ void __launch_bounds__(64 * kDecMaxWaves)
 k_brick3_decode(const uint32_t* __restrict__ bitstream, const uint8_t* __restrict__ revbook, int bklen,
                 const uint32_t* __restrict__ par_nbit, const uint32_t* __restrict__ par_entry, T* out, uint32_t lx,
                 uint32_t ly, uint32_t lz, T ebx2, T r, uint32_t nbx, uint32_t nby, uint32_t nbricks,
-                uint32_t stage_words, unsigned int* work)
+                uint32_t ahead, unsigned int* work, int dbg)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
   auto& tb = *reinterpret_cast<hfd::LdsTables<kDecB>*>(dsm);
   constexpr size_t kTabBytes = (sizeof(hfd::LdsTables<kDecB>) + 15) / 16 * 16;
   hfd::build_tables<kDecB>(tb, revbook, bklen);
+  const hfd::DecRegs rg = hfd::load_dec_regs(tb);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint32_t* stage = reinterpret_cast<uint32_t*>(dsm + kTabBytes) + (size_t)wid * (stage_words + kTileWords);
-  uint16_t* tile = reinterpret_cast<uint16_t*>(stage + stage_words);
+  constexpr uint32_t R = kRingRows;
+  uint32_t* ring = reinterpret_cast<uint32_t*>(dsm + kTabBytes) + (size_t)wid * (R * 64 + kTileWords);
+  uint16_t* tile = reinterpret_cast<uint16_t*>(ring + R * 64);
   uint16_t* myrow = tile + lane * kPitch;
   const size_t plane = (size_t)lx * ly;
   const uint32_t ubk = (uint32_t)bklen;
   constexpr uint32_t W = 64 * V;
+  // reconstruct layout: lane = (z half, column) of a 32-column block
+  const uint32_t col = lane & 31, zh = lane >> 5;
 
-  for (;;) {
-    uint32_t brick = 0;
-    if (lane == 0) brick = atomicAdd(work, 1u);
-    brick = readlane(brick, 0);
-    if (brick >= nbricks) break;
+  // bricks are handed out by kWorkShards counters (one word saturates near ~90 dequeues/us);
+  // shard q owns bricks [q per, (q + 1) per); a wave drains its home shard, then the others
+  const uint32_t per = (nbricks + kWorkShards - 1) / kWorkShards;
+  const uint32_t q0 = blockIdx.x % kWorkShards;
+  for (uint32_t qi = 0; qi < (uint32_t)kWorkShards;) {
+    const uint32_t q = (q0 + qi) % kWorkShards;
+    uint32_t got = 0;
+    if (lane == 0) got = atomicAdd(work + q * 16, 1u);
+    got = readlane(got, 0);
+    const uint32_t brick = q * per + got;
+    if (got >= per || brick >= nbricks) {
+      qi++;
+      continue;
+    }
     const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
     const uint32_t y0 = by * 8, z0 = bz * 8;
     const uint32_t ry = lane >> 3, rz = lane & 7;  // this lane's chunk = brick row (ry, rz)
@@ -360,86 +446,119 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, const uint8_t* __restric
     const uint32_t nbit = live ? par_nbit[c] : 0u;
     const uint32_t ent = live ? par_entry[c] : 0u;
     const uint32_t nc = (nbit + 31) >> 5;
-    const uint32_t inc = hfd::wave_incl_scan(nc);
-    const uint32_t soff = inc - nc, tot = readlane(inc, 63);
-    const bool staged = tot + 3 <= stage_words;
+    const uint32_t* gsrc = bitstream + ent;
+    const uint32_t top_all = wave_max(nc) + 3;  // no row is needed past every chunk's end
+    // issue rows [from, to) of the ring (LDS-DMA, lane-linear destination, per-lane source)
+    auto issue = [&](uint32_t from, uint32_t to) {
+      for (uint32_t k = from; k < to; k++) {
+        const uint32_t* g = gsrc + (k < nc ? k : 0u);
+        __builtin_amdgcn_global_load_lds(g, ring + (k & (R - 1)) * 64, 4, 0, 0);
+      }
+    };
+    uint32_t issued = min(R, min(top_all, 2 * ahead + 3));
+    issue(0, issued);
+    // compiler-visible vmcnt(0) (an asm wait would leave the waitcnt pass assuming the DMA is
+    // still in flight and make it wait inside the decode loop)
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    Ring rs{(lds_u32*)ring, issued, gsrc, nc};
     BitReader br;
-    int pend = -1;
-    if (staged) {
-      // contiguous in lane order (this encoder's layout): one coalesced block copy
-      const uint32_t e0 = readlane(ent, 0);
-      const bool contig = __builtin_amdgcn_ballot_w64(live && ent != e0 + soff) == 0;
-      if (contig) {
-        const uint32_t* src = bitstream + e0;
-        uint32_t k = lane;
-        for (; k + 7 * 64 < tot; k += 8 * 64) {
-          uint32_t v[8];
-#pragma unroll
-          for (int j = 0; j < 8; j++) v[j] = src[k + 64 * j];
-#pragma unroll
-          for (int j = 0; j < 8; j++) stage[k + 64 * j] = v[j];
-        }
-        for (; k < tot; k += 64) stage[k] = src[k];
-      }
-      else {
-        for (int j = 0; j < 64; j++) {
-          const uint32_t n = readlane(nc, j), e = readlane(ent, j), o = readlane(soff, j);
-          for (uint32_t k = lane; k < n; k += 64) stage[o + k] = bitstream[e + k];
-        }
-      }
-      if (lane < 3) stage[tot + lane] = 0u;
-      hfd::wave_sync();
-      br.buf = ((uint64_t)stage[soff] << 32) | stage[soff + 1];
-      br.avail = 64, br.nw = 2, br.nxt = stage[soff + 2];
-    }
-    else {
-      const uint32_t* src = bitstream + ent;
-      br.buf = ((uint64_t)(nc > 0 ? src[0] : 0u) << 32) | (nc > 1 ? src[1] : 0u);
-      br.avail = 64, br.nw = 2, br.nxt = nc > 2 ? src[2] : 0u;
-    }
+    br.buf = ((uint64_t)ring[lane] << 32) | ring[64 + lane];
+    br.avail = 64, br.nw = 2;
+    int carry = -1;
+    // later rows: loaded into registers one block ahead, written to the ring the block after
+    uint32_t pend[kMaxRefill];
+    uint32_t pend_from = issued, pend_cnt = 0;
 
-    for (int xb = 0; xb < V; xb++) {
-      if (staged)
-        decode_block(tb, ubk, live, br, pend, myrow, [&](uint32_t k) { return stage[soff + k]; });
-      else
-        decode_block(tb, ubk, live, br, pend, myrow,
-                     [&](uint32_t k) { return k < nc ? bitstream[ent + k] : 0u; });
+    for (int xb = 0; xb < (int)(W / kXB); xb++) {
+      if (xb > 0) {
+#pragma unroll
+        for (int j = 0; j < kMaxRefill; j++)
+          if (j < (int)pend_cnt) ring[((pend_from + j) & (R - 1)) * 64 + lane] = pend[j];
+        rs.valid_top = pend_from + pend_cnt;
+        const uint32_t lo = wave_min(live ? br.nw : 0xFFFFFFFFu);
+        const uint32_t hi = wave_max(live ? br.nw : 0u);
+        const uint32_t want = min(issued + kMaxRefill, min(top_all, min(lo + R - 1, hi + ahead)));
+        pend_from = issued;
+        pend_cnt = want > issued ? want - issued : 0u;
+#pragma unroll
+        for (int j = 0; j < kMaxRefill; j++)
+          if (j < (int)pend_cnt) {
+            const uint32_t k = issued + j;
+            pend[j] = gsrc[k < nc ? k : 0u];
+          }
+        issued += pend_cnt;
+      }
+      if (!(dbg & 1)) decode_block(tb, rg, ubk, live, br, carry, myrow, rs, lane);
       hfd::wave_sync();
-      // reconstruct the 64 columns of this block (lrz_x.cuhip.inl:311-353 order), lane = column
-      const uint32_t xg = bx * W + xb * kXB + lane;
-      T s[8];
+      if (dbg & 2) continue;  // diagnostic: no reconstruction
+      // reconstruct 32 columns (lrz_x.cuhip.inl:311-353 order): lane = (z half zh, column);
+      // z in [4 zh, 4 zh + 4) in registers, the z scan crosses halves with lane shuffles
+      const uint32_t xg = bx * W + xb * kXB + col;
+      uint16_t code[8][4];
+      T ov[8][4];
+#pragma unroll
+      for (int y = 0; y < 8; y++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t z = 4 * zh + k;
+          const bool ok = z0 + z < lz && y0 + y < ly;
+          code[y][k] = ok ? tile[(y * 8 + z) * kPitch + col] : uint16_t(1);
+          ov[y][k] = 0;
+        }
+#pragma unroll
+      for (int y = 0; y < 8; y++)
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          if (code[y][k] == 0) ov[y][k] = out[(size_t)(z0 + 4 * zh + k) * plane + (size_t)(y0 + y) * lx + xg];
+      T s[4];
+#pragma unroll
       for (int y = 0; y < 8; y++) {
         const uint32_t gy = y0 + y;
         if (gy >= ly) break;
-        T tz[8][1];
+        T tz[4][1];
 #pragma unroll
-        for (int z = 0; z < 8; z++) {
-          const bool ok = z0 + z < lz;
-          const uint16_t code = ok ? tile[(y * 8 + z) * kPitch + lane] : uint16_t(0);
-          const size_t idx = (size_t)(z0 + z) * plane + (size_t)gy * lx + xg;
-          T o = 0;
-          if (ok && code == 0) o = out[idx];
+        for (int k = 0; k < 4; k++) {
+          const bool ok = z0 + 4 * zh + k < lz;
           T v;
           if constexpr (ZZ)
-            v = ok ? o + (T)zz_dec(code) : T(0);
+            v = ok ? ov[y][k] + (T)zz_dec(code[y][k]) : T(0);
           else
-            v = ok ? (o + (T)code) - r : T(0);
-          s[z] = (y > 0) ? v + s[z] : v;
-          tz[z][0] = s[z];
+            v = ok ? (ov[y][k] + (T)code[y][k]) - r : T(0);
+          s[k] = (y > 0) ? v + s[k] : v;
+          tz[k][0] = s[k];
         }
 #pragma unroll
-        for (int z = 0; z < 8; z++) {
-          hs_step<T, 1, 8, 1>(tz[z], xg);
-          hs_step<T, 1, 8, 2>(tz[z], xg);
-          hs_step<T, 1, 8, 4>(tz[z], xg);
+        for (int k = 0; k < 4; k++) {
+          hs_step<T, 1, 8, 1>(tz[k], xg);
+          hs_step<T, 1, 8, 2>(tz[k], xg);
+          hs_step<T, 1, 8, 4>(tz[k], xg);
+        }
+        // z Hillis-Steele, d = 1, 2, 4 (descending z keeps each round's sources unmodified);
+        // the upper half reads the lower half's pre-round values
+        {
+          const T l3 = __shfl(tz[3][0], (int)col);  // lower half's t[3] (lane col)
+          tz[3][0] = tz[3][0] + tz[2][0];
+          tz[2][0] = tz[2][0] + tz[1][0];
+          tz[1][0] = tz[1][0] + tz[0][0];
+          if (zh) tz[0][0] = tz[0][0] + l3;
+        }
+        {
+          const T l2 = __shfl(tz[2][0], (int)col), l3 = __shfl(tz[3][0], (int)col);
+          tz[3][0] = tz[3][0] + tz[1][0];
+          tz[2][0] = tz[2][0] + tz[0][0];
+          if (zh) tz[1][0] = tz[1][0] + l3, tz[0][0] = tz[0][0] + l2;
+        }
+        {
+          T lo4[4];
+#pragma unroll
+          for (int k = 0; k < 4; k++) lo4[k] = __shfl(tz[k][0], (int)col);
+          if (zh)
+#pragma unroll
+            for (int k = 0; k < 4; k++) tz[k][0] = tz[k][0] + lo4[k];
         }
 #pragma unroll
-        for (int d = 1; d < 8; d *= 2)
-#pragma unroll
-          for (int z = 7; z >= d; z--) tz[z][0] = tz[z][0] + tz[z - d][0];
-#pragma unroll
-        for (int z = 0; z < 8; z++)
-          if (z0 + z < lz) out[(size_t)(z0 + z) * plane + (size_t)gy * lx + xg] = tz[z][0] * ebx2;
+        for (int k = 0; k < 4; k++)
+          if (z0 + 4 * zh + k < lz) out[(size_t)(z0 + 4 * zh + k) * plane + (size_t)gy * lx + xg] = tz[k][0] * ebx2;
       }
       hfd::wave_sync();
     }
@@ -468,11 +587,13 @@ BrickGeom brick_geom(int ndim, size_t lx, size_t ly, size_t lz, int elem_bytes)
   return g;
 }
 
-size_t brick_decode_lds(uint32_t stage_words, int waves)
+size_t brick_decode_lds(int waves)
 {
   const size_t tab = (sizeof(hfd::LdsTables<kDecB>) + 15) / 16 * 16;
-  return tab + (size_t)waves * ((size_t)stage_words + kTileWords) * 4;
+  return tab + (size_t)waves * ((size_t)kRingRows * 64 + kTileWords) * 4;
 }
+
+uint32_t brick_decode_max_ahead() { return kRingRows - 6; }
 
 int brick_configure(BrickLaunch& L, int elem_bytes, int device)
 {
@@ -480,7 +601,7 @@ int brick_configure(BrickLaunch& L, int elem_bytes, int device)
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1) ncu = 256;
   L.ncu = ncu;
   int per_scan = 0, per_pack = 0;
-  const size_t lds_scan = (size_t)kBrickWaves * kMaxBklen * 4;
+  const size_t lds_scan = (size_t)(1 + kBrickWaves) * kMaxBklen * 4;
   const size_t lds_pack = ((size_t)kMaxBklen + (size_t)kBrickWaves * pack_cells_words<4>()) * 4;
   hipError_t e1, e2;
   if (elem_bytes == 8) {
@@ -508,7 +629,7 @@ int launch_brick_scan(const BrickLaunch& L, const T* in, double eb, int radius, 
   const T ebx2_r = (T)(1.0 / (eb * 2));  // lrz_c.cuhip.inl:489
   const T r = (T)radius;
   const BrickGeom& g = L.g;
-  const size_t lds = (size_t)kBrickWaves * kMaxBklen * 4;
+  const size_t lds = (size_t)(1 + kBrickWaves) * kMaxBklen * 4;
   const int grid = L.grid_scan;
   if (zz)
     k_brick3_scan<T, 4, true><<<grid, 64 * kBrickWaves, lds, st>>>(in, L.lx, L.ly, L.lz, ebx2_r, r, ol, hist, bhist,
@@ -553,22 +674,25 @@ int launch_brick_pack(const BrickLaunch& L, const T* in, double eb, int radius, 
 template <typename T>
 int launch_brick_decode(const BrickLaunch& L, const uint32_t* bitstream, const uint8_t* revbook, int bklen,
                         const uint32_t* par_nbit, const uint32_t* par_entry, T* out, double eb, int radius, bool zz,
-                        uint32_t stage_words, int waves, unsigned int* work, hipStream_t st)
+                        uint32_t ahead, int waves, unsigned int* work, hipStream_t st)
 {
   const T ebx2 = (T)(eb * 2);  // lrz_x.cuhip.inl:432
   const T r = (T)radius;
   const BrickGeom& g = L.g;
-  const size_t lds = brick_decode_lds(stage_words, waves);
+  const size_t lds = brick_decode_lds(waves);
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
   const int grid = L.ncu;
+  // diagnostic switch (profiling only): 1 = skip the decode loop, 2 = skip the reconstruction
+  const char* dbs = getenv("CUSZ_AMD_DEC_DEBUG");
+  const int dbg = dbs ? atoi(dbs) : 0;
   if (zz)
     k_brick3_decode<T, 4, true><<<grid, 64 * waves, lds, st>>>(bitstream, revbook, bklen, par_nbit, par_entry, out,
                                                                 L.lx, L.ly, L.lz, ebx2, r, g.nbx, g.nby, g.nbricks,
-                                                                stage_words, work);
+                                                                ahead, work, dbg);
   else
     k_brick3_decode<T, 4, false><<<grid, 64 * waves, lds, st>>>(bitstream, revbook, bklen, par_nbit, par_entry, out,
                                                                  L.lx, L.ly, L.lz, ebx2, r, g.nbx, g.nby, g.nbricks,
-                                                                 stage_words, work);
+                                                                 ahead, work, dbg);
   return (int)hipGetLastError();
 }
 

@@ -100,17 +100,35 @@ __device__ __forceinline__ uint32_t tab_decode1(uint32_t v, const uint32_t* firs
   return l;
 }
 
-// Decode tables resident in LDS: L1 (2^B entries), keys, base[l] = entry[l] - first[l],
-// first[l] for the slow path (codes longer than B bits).
+// Decode tables resident in LDS.
+//  L1: 2^B entries indexed by the next B bits, one or two whole codewords of <= B bits.
+//  L2: single-symbol entries indexed DIRECTLY by the next 16 bits.  Canonical codes put every
+//      code longer than B bits below first[B] (longer codes are numerically smaller), so only
+//      windows whose B-bit prefix is < first[B] reach it: first[B] << (16 - B) entries (capped;
+//      its last entry stays 0).  L1 and L2 are read together, so a 12..16-bit code costs no
+//      extra round trip.
+//  Codes longer than 16 bits (or past the cap) count failing lengths against thresholds the
+//  caller keeps in registers (DecRegs).
+constexpr int kL2Bits = 16;
+constexpr int kL2Cap = 4096;
+
 template <int B>
 struct LdsTables {
   uint32_t l1[1 << B];
+  uint32_t l2[kL2Cap];
   uint32_t first[32];
   uint32_t base[32];
   uint32_t entry[32];
   uint32_t maxl;
   uint32_t pad[3];
   uint16_t keys[kMaxBklen];
+};
+
+// wave-uniform thresholds for the rare untabulated codes (first[l], l = 12..27)
+constexpr int kSlowFrom = 12;
+struct DecRegs {
+  uint32_t first[kLmax - kSlowFrom + 1];
+  uint32_t maxl;
 };
 
 // Cooperative build by the whole workgroup (ends with a barrier).
@@ -129,31 +147,60 @@ __device__ __forceinline__ void build_tables(LdsTables<B>& t, const uint8_t* rev
     if (tid == 0) t.maxl = (uint32_t)maxl;
   }
   __syncthreads();
+  uint32_t first[32];  // registers: the unrolled threshold loop reads no LDS
+#pragma unroll
+  for (int k = 0; k < 32; k++) first[k] = t.first[k];
+  const uint32_t* base = t.base;
+  const uint32_t ub = (uint32_t)bklen;
   for (uint32_t i = tid; i < (1u << B); i += nt) {
     const uint32_t v = i << (32 - B);
     uint32_t s0, s1, e = 0;
-    const uint32_t l0 = tab_decode1(v, t.first, maxl, t.base, t.keys, (uint32_t)bklen, s0);
+    const uint32_t l0 = tab_decode1(v, first, maxl, base, t.keys, ub, s0);
     if (l0 <= (uint32_t)B) {
       const uint32_t rest = B - l0;
-      const uint32_t l1 = rest ? tab_decode1(v << l0, t.first, maxl, t.base, t.keys, (uint32_t)bklen, s1) : 99u;
+      const uint32_t l1 = rest ? tab_decode1(v << l0, first, maxl, base, t.keys, ub, s1) : 99u;
       e = l1 <= rest ? lut_pack(2, l0 + l1, l0, s0, s1) : lut_pack(1, l0, l0, s0, 0);
     }
     t.l1[i] = e;
   }
+  const uint32_t P = maxl > B ? min(first[B], 1u << B) : 0u;
+  const uint32_t n2 = min(P << (kL2Bits - B), (uint32_t)kL2Cap - 1);
+  for (uint32_t q = tid; q < (uint32_t)kL2Cap; q += nt) {
+    uint32_t e = 0;
+    if (q < n2) {
+      uint32_t s0;
+      const uint32_t l = tab_decode1(q << (32 - kL2Bits), first, maxl, base, t.keys, ub, s0);
+      if (l <= (uint32_t)kL2Bits) e = lut_pack(1, l, l, s0, 0);
+    }
+    t.l2[q] = e;
+  }
   __syncthreads();
 }
 
-// Entry for the codeword(s) at the top of `win`; codes longer than B bits are resolved by
-// counting failing lengths (all lengths <= B failed).
 template <int B>
-__device__ __forceinline__ uint32_t lookup(const LdsTables<B>& t, uint32_t win, uint32_t bklen)
+__device__ __forceinline__ DecRegs load_dec_regs(const LdsTables<B>& t)
 {
-  uint32_t e = t.l1[win >> (32 - B)];
-  if (__builtin_expect(!(e >> 30), 0)) {
-    const uint32_t maxl = t.maxl;
+  static_assert(B + 1 >= kSlowFrom, "slow path thresholds start at B + 1");
+  DecRegs r;
+#pragma unroll
+  for (int q = 0; q < kLmax - kSlowFrom + 1; q++) r.first[q] = __builtin_amdgcn_readfirstlane(t.first[kSlowFrom + q]);
+  r.maxl = __builtin_amdgcn_readfirstlane(t.maxl);
+  return r;
+}
+
+// Entry for the codeword(s) at the top of `win`.
+template <int B>
+__device__ __forceinline__ uint32_t lookup(const LdsTables<B>& t, const DecRegs& rg, uint32_t win, uint32_t bklen)
+{
+  const uint32_t e1 = t.l1[win >> (32 - B)];
+  const uint32_t e2 = t.l2[min(win >> (32 - kL2Bits), (uint32_t)kL2Cap - 1)];
+  uint32_t e = (e1 >> 30) ? e1 : e2;
+  if (__builtin_expect(!(e >> 30), 0)) {  // all lengths <= B failed: count the rest
     uint32_t l = B + 1;
-    for (uint32_t k = B + 1; k < maxl; k++) l += (win >> (32 - k)) < t.first[k] ? 1u : 0u;
-    if (l > maxl) l = maxl;
+#pragma unroll
+    for (int q = B + 1 - kSlowFrom; q < kLmax - kSlowFrom + 1; q++)
+      l += (kSlowFrom + q < (int)rg.maxl && (win >> (32 - (kSlowFrom + q))) < rg.first[q]) ? 1u : 0u;
+    if (l > rg.maxl) l = rg.maxl;
     const uint32_t s = t.keys[min(t.base[l] + (win >> (32 - l)), bklen - 1)];
     e = lut_pack(1, l, l, s, 0);
   }

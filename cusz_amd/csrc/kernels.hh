@@ -180,8 +180,9 @@ struct BrickLaunch {
 // fills ncu and the encode-pass grids for `device`
 int brick_configure(BrickLaunch& L, int elem_bytes, int device);
 
-// LDS bytes of the fused decoder for `waves` waves with `stage_words` staging words each
-size_t brick_decode_lds(uint32_t stage_words, int waves);
+// LDS bytes of the fused decoder for `waves` waves; the largest look-ahead (ring rows) it takes
+size_t brick_decode_lds(int waves);
+uint32_t brick_decode_max_ahead();
 
 template <typename T>
 int launch_brick_scan(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const OutlierSink& ol,
@@ -195,7 +196,7 @@ int launch_brick_pack(const BrickLaunch& L, const T* in, double eb, int radius, 
 template <typename T>
 int launch_brick_decode(const BrickLaunch& L, const uint32_t* bitstream, const uint8_t* revbook, int bklen,
                         const uint32_t* par_nbit, const uint32_t* par_entry, T* out, double eb, int radius, bool zz,
-                        uint32_t stage_words, int waves, unsigned int* work, hipStream_t st);
+                        uint32_t ahead, int waves, unsigned int* work, hipStream_t st);
 
 // min / max (Rel mode, extrema.cuhip.inl:86-208), writes {min, max} as doubles
 template <typename T>

@@ -134,7 +134,8 @@ struct Pipeline {
   double* minmax() { return reinterpret_cast<double*>(d_small + 256); }
   unsigned int* ext_scratch() { return reinterpret_cast<unsigned int*>(d_small + 512); }
   uint32_t* dec_lut() { return reinterpret_cast<uint32_t*>(d_small + 512 + 2 * 1024 * 8); }
-  static constexpr size_t kSmallBytes = 512 + 2 * 1024 * 8 + kHfDecScratchWords * 4;
+  static constexpr size_t kWorkBytes = 512;  // fused decoder work counters (8 shards x 64 B)
+  static constexpr size_t kSmallBytes = 512 + 2 * 1024 * 8 + kHfDecScratchWords * 4 + kWorkBytes;
 
   ~Pipeline() { release(); }
 
@@ -159,7 +160,7 @@ struct Pipeline {
 
   size_t rvbk_bytes(int bklen) const { return 4 * 64 + 2 * (size_t)bklen; }
   uint32_t brick_cap() const { return bl.g.brick_elems / 10 + 16; }
-  unsigned int* work_counter() { return reinterpret_cast<unsigned int*>(d_small + 32); }
+  unsigned int* work_counter() { return reinterpret_cast<unsigned int*>(d_small + kSmallBytes - kWorkBytes); }
 
   // fused brick path: 3-D, eligible shape, Lorenzo, default chunking (chunk = brick row)
   bool use_brick(psz_predictor pred) const
@@ -555,19 +556,18 @@ struct Pipeline {
     const size_t seg = h->entry[PSZHEADER_ENCODED + 1] - h->entry[PSZHEADER_ENCODED];
     const size_t fixed = 128 + rvbk + 8 * (size_t)pd;
     const size_t cells = seg > fixed ? (seg - fixed) / 4 : 0;
-    // LDS staging per wave: the average brick plus margin (bricks above it decode from HBM)
-    const size_t worst = (size_t)bl.g.brick_elems * kLmax / 32 + 64 + 4;
-    size_t stage = cells / std::max<uint32_t>(bl.g.nbricks, 1);
-    stage = std::min(worst, stage + stage / 4 + 96);
-    stage = (stage + 3) / 4 * 4;
-    int waves = 8;
-    while (waves > 1 && brick_decode_lds((uint32_t)stage, waves) > 160 * 1024) waves--;
-    if (brick_decode_lds((uint32_t)stage, waves) > 160 * 1024) stage = 1024;  // tiny stage, HBM reads
-    CUSZ_AMD_HIP_CHECK(hipMemsetAsync(work_counter(), 0, 4, stream));
+    // input ring per wave: rows (words of every chunk) issued one 32-symbol block ahead; sized
+    // from the archive's average bits per symbol (a lane that outruns the ring reads HBM)
+    const double words_per_block = (double)cells / std::max<size_t>(pd, 1) * 32.0 / bl.g.W;
+    uint32_t ahead = (uint32_t)(2.4 * words_per_block) + 4;
+    ahead = std::min(ahead, brick_decode_max_ahead());
+    int waves = 12;  // kDecMaxWaves
+    while (waves > 1 && brick_decode_lds(waves) > 160 * 1024) waves--;
+    CUSZ_AMD_HIP_CHECK(hipMemsetAsync(work_counter(), 0, kWorkBytes, stream));
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_decode<T>(
         bl, reinterpret_cast<const uint32_t*>(phf + 128 + rvbk + 8 * (size_t)pd), phf + 128, bklen,
         reinterpret_cast<const uint32_t*>(phf + 128 + rvbk), reinterpret_cast<const uint32_t*>(phf + 128 + rvbk + 4 * (size_t)pd),
-        out, h->rc.eb, h->rc.radius, zz, (uint32_t)stage, waves, work_counter(), stream));
+        out, h->rc.eb, h->rc.radius, zz, ahead, waves, work_counter(), stream));
     mark(8);
     mark(9);
     return PSZ_SUCCESS;
