@@ -36,13 +36,7 @@ using namespace lrzd;
 namespace {
 
 constexpr int kBrickWaves = 4;  // waves per workgroup in the encode passes
-constexpr int kDecB = 11;       // decode table index bits
-constexpr int kXB = 32;         // decode x-block (symbols per chunk per step = columns reconstructed)
-constexpr int kPitch = 40;      // LDS code tile row pitch (u16): rows 4 apart are 16 banks apart
-constexpr int kTileWords = 64 * kPitch / 2;
-constexpr int kWorkShards = 8;
-constexpr uint32_t kRingRows = 32;  // decoder input ring rows (power of two): 8 KB per wave
-constexpr int kMaxRefill = 12;      // ring rows refilled per 32-symbol block (registers)  // decoder work counters, 64 B apart (kBrickWorkWords words)
+constexpr int kWorkShards = 8;  // decoder work counters, 64 B apart
 
 __device__ __forceinline__ uint32_t readlane(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
 
@@ -317,117 +311,217 @@ k_brick3_pack(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
 // =========================================================================================
 // decompress: chunk decode + reconstruct, one wave per brick
 // =========================================================================================
-// Input staging.  Lane l decodes chunk l (brick row (y, z) = (l / 8, l % 8)).  The words of all
-// 64 chunks are staged in an LDS ring laid out [word k][lane]: row k holds word k of every chunk,
-// filled by one LDS-DMA instruction with per-lane source addresses (lane-linear destination),
-// so a lane's reads ring[(k % R) * 64 + lane] never conflict.  Rows are issued a block ahead and
-// land while the current block decodes; a lane that outruns the resident rows reads HBM.
-struct BitReader {
-  uint64_t buf;    // next bits of the chunk, left-justified
-  uint32_t avail;  // valid bits in buf (>= 32 between steps)
-  uint32_t nw;     // index of the next chunk word to append
-};
-
-// LDS pointer type: keeps ring reads ds_read_* (a generic pointer that may alias global memory
-// would become a flat load, which waits on every outstanding DMA and store)
-using lds_u32 = __attribute__((address_space(3))) const uint32_t;
-
-struct Ring {
-  lds_u32* ring;         // this wave's kRingRows x 64 words, row k % kRingRows holds chunk word k
-  uint32_t valid_top;    // rows [.., valid_top) have landed
-  const uint32_t* gsrc;  // this lane's chunk in HBM (fallback past the resident rows)
-  uint32_t nc;           // words in this lane's chunk
-};
-
-// A chunk word the ring does not hold yet, read from HBM.  The load and its wait are inline asm
-// so the compiler's wait insertion does not place a vmcnt(0) -- which would also wait for every
-// in-flight ring DMA and output store -- at the join after this rare branch on the common path.
-__device__ __forceinline__ uint32_t fallback_word(const Ring& rs, uint32_t k)
-{
-  if (k >= rs.nc) return 0u;
-  uint32_t v;
-  asm volatile("global_load_dword %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(rs.gsrc + k) : "memory");
-  return v;
-}
-
-// decode kXB symbols of this lane's chunk into its tile row (plus a carried symbol when a
-// two-symbol step crossed the previous block's end; the row has slack for the overrun).
-// Branch-free step: the L1/L2 entries and the next input word are read together; a finished
-// lane keeps stepping with a zero length (no state change) until the whole wave is done.
-__device__ __forceinline__ void decode_block(const hfd::LdsTables<kDecB>& tb, const hfd::DecRegs& rg, uint32_t bklen,
-                                             bool live, BitReader& br, int& carry, uint16_t* row, const Ring& rs,
-                                             int lane)
-{
-  uint32_t cnt = 0;
-  if (carry >= 0) row[0] = (uint16_t)carry, cnt = 1;
-  carry = -1;
-  if (!live) cnt = kXB + 1;
-  while (__builtin_amdgcn_ballot_w64(cnt < kXB)) {
-#pragma unroll
-    for (int st = 0; st < 4; st++) {
-      const uint32_t win = (uint32_t)(br.buf >> 32);
-      uint32_t nxt = rs.ring[(br.nw & (kRingRows - 1)) * 64 + lane];
-      if (__builtin_expect(br.nw >= rs.valid_top, 0)) nxt = fallback_word(rs, br.nw);
-      const uint32_t e = hfd::lookup<kDecB>(tb, rg, win, bklen);
-      const bool act = cnt < kXB;
-      const uint32_t c = min(cnt, (uint32_t)kXB + 1);
-      row[c] = (uint16_t)(e & 1023u);
-      row[c + 1] = (uint16_t)((e >> 10) & 1023u);  // overwritten next step unless two symbols
-      const uint32_t l = act ? ((e >> 25) & 31u) : 0u;  // bits consumed (1 or 2 codes)
-      cnt += act ? (e >> 30) : 0u;
-      br.buf <<= l;
-      br.avail -= l;
-      const bool rf = br.avail < 32;
-      br.buf |= rf ? ((uint64_t)nxt << (32 - br.avail)) : 0ull;
-      br.avail += rf ? 32u : 0u;
-      br.nw += rf ? 1u : 0u;
-    }
-  }
-  if (cnt == kXB + 1 && live) carry = row[kXB];
-}
+// Lane l decodes chunk l of the brick (brick row (y, z) = (l / 8, l % 8)), 32 symbols per
+// sub-block, into an LDS code tile [row][column]; every 64 columns the wave reconstructs the
+// block with lane = column (y running sums and z Hillis-Steele in registers, x Hillis-Steele
+// across lanes by DPP) and stores whole 256-B rows.
+//
+// Input ring.  Row k of a wave's ring holds word k of all 64 chunks ([word][lane]: a lane's
+// reads never conflict), rows in descending slots with a copy of row 0 below the first slot,
+// so that the pair (k, k + 1) is always one ds_read2 that lands as the 64-bit value {k : k+1}.  Rows are loaded by buffer loads (range-checked against the
+// bitstream, per-lane chunk offset in the VGPR offset, row in the SGPR offset) one sub-block
+// ahead and written to the ring at the next sub-block; a lane that outruns the resident rows
+// reads HBM.  The decode step keeps only a bit position: peek 32 bits at `pos` from the word
+// pair, look up one or two codes, store them, advance.
+#ifndef CUSZ_AMD_DEC_B  // tuning knobs (overridable at build time for experiments)
+#define CUSZ_AMD_DEC_B 11
+#endif
+#ifndef CUSZ_AMD_DEC_RING
+#define CUSZ_AMD_DEC_RING 16
+#endif
+#ifndef CUSZ_AMD_DEC_PF
+#define CUSZ_AMD_DEC_PF 8
+#endif
+#ifndef CUSZ_AMD_DEC_STEPS
+#define CUSZ_AMD_DEC_STEPS 4
+#endif
+#ifndef CUSZ_AMD_DEC_REFILL
+#define CUSZ_AMD_DEC_REFILL 4
+#endif
+constexpr int kDecB = CUSZ_AMD_DEC_B;            // L1 decode table index bits
+constexpr int kSteps = CUSZ_AMD_DEC_STEPS;       // decode steps per loop iteration
+constexpr int kRefillEvery = CUSZ_AMD_DEC_REFILL;  // loop iterations between ring refills (power of 2)
+constexpr int kBlk = 64;                         // columns reconstructed per block (= lanes)
+constexpr int kTP = kBlk + 2;                    // tile row pitch (u16): row r starts at bank r
+constexpr uint32_t kRing = CUSZ_AMD_DEC_RING;    // ring rows (chunk words per lane), power of two
+constexpr int kPF = CUSZ_AMD_DEC_PF;             // ring rows loaded per sub-block at most
+constexpr uint32_t kRingWords = (kRing + 1) * 64;
+constexpr size_t kDecWaveBytes = kRingWords * 4 + (size_t)64 * kTP * 2;
+constexpr int kDecMaxWaves = 12;
+constexpr uint32_t kBufRsrcW3 = 0x00020000;     // raw buffer resource word 3 (gfx9)
 
 __device__ __forceinline__ uint32_t wave_min(uint32_t v)
 {
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) v = min(v, (uint32_t)__shfl_xor(v, d));
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);  // uniform: keep it in an SGPR
+}
+__device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v)
+{
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d);
   return v;
 }
 __device__ __forceinline__ uint32_t wave_max(uint32_t v)
 {
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d));
-  return v;
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
 
-constexpr int kDecMaxWaves = 12;  // 3 waves per SIMD: up to 168 VGPRs without spills
-
-template <typename T, int V, bool ZZ>
-__global__ void __launch_bounds__(64 * kDecMaxWaves)
-k_brick3_decode(const uint32_t* __restrict__ bitstream, const uint8_t* __restrict__ revbook, int bklen,
-                const uint32_t* __restrict__ par_nbit, const uint32_t* __restrict__ par_entry, T* out, uint32_t lx,
-                uint32_t ly, uint32_t lz, T ebx2, T r, uint32_t nbx, uint32_t nby, uint32_t nbricks,
-                uint32_t ahead, unsigned int* work, int dbg)
+// Chunk words k, k + 1 from HBM for a lane past the resident ring rows (rare).  The loads and
+// their wait are inline asm: a compiler-visible load here would make the waitcnt pass place a
+// vmcnt(0) -- which also waits for every in-flight ring load and output store -- at the join.
+__device__ __forceinline__ void fallback_pair(const uint32_t* g, uint32_t k, uint32_t lim, uint32_t& w0, uint32_t& w1)
 {
+  const uint32_t* p0 = g + (k < lim ? k : lim - 1u);
+  const uint32_t* p1 = g + (k + 1u < lim ? k + 1u : lim - 1u);
+  asm volatile("global_load_dword %0, %2, off\n\tglobal_load_dword %1, %3, off\n\ts_waitcnt vmcnt(0)"
+               : "=&v"(w0), "=&v"(w1)
+               : "v"(p0), "v"(p1)
+               : "memory");
+}
+
+// x Hillis-Steele inside 8-wide tiles across lanes (lrz_x.cuhip.inl:311-353 order: d = 1, 2, 4;
+// t += t[lane - d] when lane % 8 >= d).  d = 1, 2: the source is zeroed on the lanes whose
+// value would cross into the next tile, so the DPP add is unconditional (t + 0 == t: no -0
+// arises in the reconstruction); d = 4: the bank mask keeps lanes 4-7 and 12-15 of each row.
+template <int CTRL, int BANK>
+__device__ __forceinline__ float dppf(float v)
+{
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, BANK, false));
+}
+template <int CTRL, int BANK>
+__device__ __forceinline__ double dppf(double v)
+{
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xf, BANK, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xf, BANK, false);
+  return __builtin_bit_cast(double, (unsigned long long)(uint32_t)lo | ((unsigned long long)(uint32_t)hi << 32));
+}
+template <typename T>
+__device__ __forceinline__ T x_scan8(T t, uint32_t l7)
+{
+  t = t + dppf<0x111, 0xf>(l7 == 7 ? T(0) : t);
+  t = t + dppf<0x112, 0xf>(l7 >= 6 ? T(0) : t);
+  t = t + dppf<0x114, 0xa>(t);
+  return t;
+}
+
+template <typename T>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const T* base)
+{
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(base), 0, (int)0xFFFFFFFF, (int)kBufRsrcW3);
+}
+template <typename T>
+__device__ __forceinline__ void buf_store(T v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff);
+template <>
+__device__ __forceinline__ void buf_store<float>(float v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff)
+{
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)voff, (int)soff, 0);
+}
+template <>
+__device__ __forceinline__ void buf_store<double>(double v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff)
+{
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, (int)voff, (int)soff, 0);
+}
+
+// Reconstruct columns [xg0, xg0 + 64) of the brick from the code tile (lane = column).
+// lrz_x.cuhip.inl:271-360 order: v = (outlier + code) - r; y running sum (sequential); x then z
+// Hillis-Steele; times 2 eb.  `out` holds the scattered outlier values (read where code == 0).
+template <typename T, bool ZZ, bool BUF>
+__device__ __forceinline__ void recon_block(const uint16_t* tile, T* out, size_t plane, uint32_t lx, uint32_t nyv,
+                                            uint32_t nzv, size_t base_elem, T r, T ebx2, int lane)
+{
+  T* base = out + base_elem;  // element (x0, y0, z0) of this block
+  const __amdgpu_buffer_rsrc_t ro = rsrc(base);
+  const uint32_t voff = (uint32_t)lane * sizeof(T);
+  const uint32_t l7 = (uint32_t)lane & 7u;
+  T s[8];
+#pragma unroll
+  for (int y = 0; y < 8; y++) {
+    if ((uint32_t)y >= nyv) break;
+    uint32_t cd[8];
+#pragma unroll
+    for (int z = 0; z < 8; z++) cd[z] = tile[(y * 8 + z) * kTP + lane];
+    T v[8];
+    bool anyz = false;
+#pragma unroll
+    for (int z = 0; z < 8; z++) {
+      if constexpr (ZZ)
+        v[z] = (T)zz_dec((uint16_t)cd[z]);
+      else
+        v[z] = (T)cd[z] - r;
+      anyz |= cd[z] == 0u;
+    }
+    if (__builtin_amdgcn_ballot_w64(anyz)) {  // outliers: their values were scattered into out
+#pragma unroll
+      for (int z = 0; z < 8; z++)
+        if (cd[z] == 0u && (uint32_t)z < nzv) {
+          const T ov = base[(size_t)z * plane + (size_t)y * lx + lane];
+          v[z] = ZZ ? ov + T(0) : ov - r;
+        }
+    }
+    T t[8];
+#pragma unroll
+    for (int z = 0; z < 8; z++) {
+      s[z] = y > 0 ? s[z] + v[z] : v[z];
+      t[z] = x_scan8<T>(s[z], l7);
+    }
+#pragma unroll
+    for (int d = 1; d < 8; d *= 2)
+#pragma unroll
+      for (int z = 7; z >= d; z--) t[z] = t[z] + t[z - d];
+#pragma unroll
+    for (int z = 0; z < 8; z++) {
+      if ((uint32_t)z >= nzv) break;
+      const T o = t[z] * ebx2;
+      if constexpr (BUF)
+        buf_store<T>(o, ro, voff, (uint32_t)(((size_t)z * plane + (size_t)y * lx) * sizeof(T)));
+      else
+        base[(size_t)z * plane + (size_t)y * lx + lane] = o;
+    }
+  }
+}
+
+#ifdef CUSZ_AMD_DEC_PROFILE
+// diagnostic build: per-phase clocks and counts summed over waves (psz_amd_debug_brick_profile)
+// 0 bricks, 1 brick cycles, 2 setup cycles, 3 decode cycles, 4 recon cycles, 5 decode loop
+// iterations, 6 fallback lane-steps, 7 idle cycles (work counter), 8 rows loaded
+__device__ unsigned long long g_brick_prof[16];
+#define BPROF(...) __VA_ARGS__
+#else
+#define BPROF(...)
+#endif
+
+template <typename T, bool ZZ, bool BUF>
+__global__ void __launch_bounds__(64 * kDecMaxWaves)
+k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const uint8_t* __restrict__ revbook,
+                int bklen, const uint32_t* __restrict__ par_nbit, const uint32_t* __restrict__ par_entry, T* out,
+                uint32_t lx, uint32_t ly, uint32_t lz, T ebx2, T r, uint32_t nbx, uint32_t nby, uint32_t nbricks,
+                uint32_t ahead, unsigned int* work)
+{
+  __shared__ hfd::LdsTables<kDecB> tb;  // static: table addresses fold into the ds offsets
   extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
-  auto& tb = *reinterpret_cast<hfd::LdsTables<kDecB>*>(dsm);
-  constexpr size_t kTabBytes = (sizeof(hfd::LdsTables<kDecB>) + 15) / 16 * 16;
   hfd::build_tables<kDecB>(tb, revbook, bklen);
   const hfd::DecRegs rg = hfd::load_dec_regs(tb);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  constexpr uint32_t R = kRingRows;
-  uint32_t* ring = reinterpret_cast<uint32_t*>(dsm + kTabBytes) + (size_t)wid * (R * 64 + kTileWords);
-  uint16_t* tile = reinterpret_cast<uint16_t*>(ring + R * 64);
-  uint16_t* myrow = tile + lane * kPitch;
+  uint32_t* ring = reinterpret_cast<uint32_t*>(dsm + (size_t)wid * kDecWaveBytes);
+  uint16_t* tile = reinterpret_cast<uint16_t*>(ring + kRingWords);
+  // logical ring row L lives in slot kRing - (L % kRing); slot 0 repeats the rows L % kRing == 0,
+  // so rows k + 1 and k always sit in adjacent slots (k + 1 below)
+  const uint32_t* ring_lane = ring + kRing * 64 + lane;
+  const __amdgpu_buffer_rsrc_t rbits =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(bitstream), 0, (int)(bs_words * 4u), (int)kBufRsrcW3);
   const size_t plane = (size_t)lx * ly;
   const uint32_t ubk = (uint32_t)bklen;
-  constexpr uint32_t W = 64 * V;
-  // reconstruct layout: lane = (z half, column) of a 32-column block
-  const uint32_t col = lane & 31, zh = lane >> 5;
+  constexpr uint32_t W = 256;
 
-  // bricks are handed out by kWorkShards counters (one word saturates near ~90 dequeues/us);
-  // shard q owns bricks [q per, (q + 1) per); a wave drains its home shard, then the others
+  // bricks are handed out by kWorkShards counters; shard q owns bricks [q per, (q + 1) per)
   const uint32_t per = (nbricks + kWorkShards - 1) / kWorkShards;
   const uint32_t q0 = blockIdx.x % kWorkShards;
+  BPROF(unsigned long long pc[9] = {}; unsigned long long tk = __builtin_readcyclecounter(), t0 = tk;)
   for (uint32_t qi = 0; qi < (uint32_t)kWorkShards;) {
     const uint32_t q = (q0 + qi) % kWorkShards;
     uint32_t got = 0;
@@ -438,131 +532,105 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, const uint8_t* __restric
       qi++;
       continue;
     }
+    BPROF(tk = __builtin_readcyclecounter(); pc[7] += tk - t0; t0 = tk; pc[0]++;)
     const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
     const uint32_t y0 = by * 8, z0 = bz * 8;
-    const uint32_t ry = lane >> 3, rz = lane & 7;  // this lane's chunk = brick row (ry, rz)
+    const uint32_t ry = (uint32_t)lane >> 3, rz = (uint32_t)lane & 7u;
     const bool live = y0 + ry < ly && z0 + rz < lz;
     const size_t c = ((size_t)(z0 + rz) * ly + (y0 + ry)) * nbx + bx;
     const uint32_t nbit = live ? par_nbit[c] : 0u;
     const uint32_t ent = live ? par_entry[c] : 0u;
-    const uint32_t nc = (nbit + 31) >> 5;
+    const uint32_t voff = ent * 4u;
     const uint32_t* gsrc = bitstream + ent;
-    const uint32_t top_all = wave_max(nc) + 3;  // no row is needed past every chunk's end
-    // issue rows [from, to) of the ring (LDS-DMA, lane-linear destination, per-lane source)
-    auto issue = [&](uint32_t from, uint32_t to) {
-      for (uint32_t k = from; k < to; k++) {
-        const uint32_t* g = gsrc + (k < nc ? k : 0u);
-        __builtin_amdgcn_global_load_lds(g, ring + (k & (R - 1)) * 64, 4, 0, 0);
-      }
-    };
-    uint32_t issued = min(R, min(top_all, 2 * ahead + 3));
-    issue(0, issued);
-    // compiler-visible vmcnt(0) (an asm wait would leave the waitcnt pass assuming the DMA is
-    // still in flight and make it wait inside the decode loop)
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-    Ring rs{(lds_u32*)ring, issued, gsrc, nc};
-    BitReader br;
-    br.buf = ((uint64_t)ring[lane] << 32) | ring[64 + lane];
-    br.avail = 64, br.nw = 2;
-    int carry = -1;
-    // later rows: loaded into registers one block ahead, written to the ring the block after
-    uint32_t pend[kMaxRefill];
-    uint32_t pend_from = issued, pend_cnt = 0;
+    const uint32_t glim = bs_words > ent ? bs_words - ent : 1u;
 
-    for (int xb = 0; xb < (int)(W / kXB); xb++) {
-      if (xb > 0) {
+    // initial ring: rows [0, kRing) of every chunk
+    {
+      uint32_t v[kRing];
 #pragma unroll
-        for (int j = 0; j < kMaxRefill; j++)
-          if (j < (int)pend_cnt) ring[((pend_from + j) & (R - 1)) * 64 + lane] = pend[j];
-        rs.valid_top = pend_from + pend_cnt;
-        const uint32_t lo = wave_min(live ? br.nw : 0xFFFFFFFFu);
-        const uint32_t hi = wave_max(live ? br.nw : 0u);
-        const uint32_t want = min(issued + kMaxRefill, min(top_all, min(lo + R - 1, hi + ahead)));
-        pend_from = issued;
-        pend_cnt = want > issued ? want - issued : 0u;
+      for (uint32_t k = 0; k < kRing; k++) v[k] = __builtin_amdgcn_raw_buffer_load_b32(rbits, (int)voff, (int)(k * 4), 0);
 #pragma unroll
-        for (int j = 0; j < kMaxRefill; j++)
-          if (j < (int)pend_cnt) {
-            const uint32_t k = issued + j;
-            pend[j] = gsrc[k < nc ? k : 0u];
+      for (uint32_t k = 0; k < kRing; k++) ring[(kRing - k) * 64 + lane] = v[k];
+      ring[lane] = v[0];
+    }
+    // per-lane window: rows [ctop - kRing, ctop) resident, rows [ctop, ltop) in flight
+    uint32_t ctop = kRing, ltop = kRing, vt_bits = (kRing - 1u) * 32u;
+    const uint32_t need_top = ((nbit + 31u) >> 5) + 1u;  // the peek pair reads one word past the end
+    uint32_t pos = 0, cnt = live ? 0u : 0x40000000u;  // a dead lane never steps
+    uint32_t pend[kPF];
+    BPROF(hfd::wave_sync(); tk = __builtin_readcyclecounter(); pc[2] += tk - t0; unsigned long long tp = tk;)
+    // Refill, per lane: write the rows loaded at the previous refill into the ring, then load
+    // up to kPF more -- never past the chunk's end, never over a row the lane still needs (row
+    // k replaces row k - kRing; the lane reads from pos / 32 on).
+    auto refill = [&]() {
+#pragma unroll
+      for (int j = 0; j < kPF; j++)
+        if (ctop + j < ltop) {
+          const uint32_t ph = (ctop + j) & (kRing - 1u);
+          ring[(kRing - ph) * 64 + lane] = pend[j];
+          if (ph == 0) ring[lane] = pend[j];
+        }
+      ctop = ltop;
+      vt_bits = (ctop - 1u) * 32u;  // pos >= vt_bits: the word pair at pos is not resident
+      const uint32_t lim = min(need_top, (pos >> 5) + kRing - 1u);
+      const uint32_t nload = lim > ltop ? min(lim - ltop, (uint32_t)kPF) : 0u;
+      const uint32_t lvoff = voff + ltop * 4u;
+#pragma unroll
+      for (int j = 0; j < kPF; j++)
+        if ((uint32_t)j < nload) pend[j] = __builtin_amdgcn_raw_buffer_load_b32(rbits, (int)lvoff, j * 4, 0);
+      BPROF(pc[8] += wave_sum64(nload);)
+      ltop += nload;
+    };
+
+    for (int blk = 0; blk < (int)(W / kBlk); blk++) {
+      uint16_t* rowp = tile + lane * kTP - blk * kBlk;  // rowp[cnt] = tile column cnt - 64 blk
+      const uint32_t target = (uint32_t)(blk + 1) * kBlk;
+      refill();
+      uint32_t it = 0;
+      do {
+#pragma unroll
+        for (int st = 0; st < kSteps; st++)
+          if (cnt < target) {
+            // rows k and k + 1 are adjacent slots, k + 1 below k: one ds_read2 gives {w1, w0}
+            const uint32_t* pr = ring_lane - ((pos >> 5) & (kRing - 1u)) * 64;
+            uint32_t w1 = pr[-64], w0 = pr[0];
+            if (__builtin_expect(pos >= vt_bits, 0)) {
+              fallback_pair(gsrc, pos >> 5, glim, w0, w1);
+              BPROF(pc[6]++;)
+            }
+            const uint64_t pair = ((uint64_t)w0 << 32) | w1;
+            const uint32_t win = (uint32_t)((pair << (pos & 31u)) >> 32);  // chunk bits [pos, pos + 32)
+            const uint32_t e = hfd::lookup<kDecB>(tb, rg, win, ubk);
+            // both symbols with one (2-B aligned) 32-bit store; the second is overwritten next
+            // step unless the entry holds two
+            *reinterpret_cast<uint32_t*>(rowp + cnt) = e & hfd::kEntSymMask;
+            pos += hfd::ent_bits(e);
+            cnt += hfd::ent_nsym(e);
           }
-        issued += pend_cnt;
-      }
-      if (!(dbg & 1)) decode_block(tb, rg, ubk, live, br, carry, myrow, rs, lane);
+        BPROF(pc[5]++;)
+        if ((++it & (kRefillEvery - 1)) == 0) refill();
+      } while (__builtin_amdgcn_ballot_w64(cnt < target));
       hfd::wave_sync();
-      if (dbg & 2) continue;  // diagnostic: no reconstruction
-      // reconstruct 32 columns (lrz_x.cuhip.inl:311-353 order): lane = (z half zh, column);
-      // z in [4 zh, 4 zh + 4) in registers, the z scan crosses halves with lane shuffles
-      const uint32_t xg = bx * W + xb * kXB + col;
-      uint16_t code[8][4];
-      T ov[8][4];
-#pragma unroll
-      for (int y = 0; y < 8; y++)
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const uint32_t z = 4 * zh + k;
-          const bool ok = z0 + z < lz && y0 + y < ly;
-          code[y][k] = ok ? tile[(y * 8 + z) * kPitch + col] : uint16_t(1);
-          ov[y][k] = 0;
-        }
-#pragma unroll
-      for (int y = 0; y < 8; y++)
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-          if (code[y][k] == 0) ov[y][k] = out[(size_t)(z0 + 4 * zh + k) * plane + (size_t)(y0 + y) * lx + xg];
-      T s[4];
-#pragma unroll
-      for (int y = 0; y < 8; y++) {
-        const uint32_t gy = y0 + y;
-        if (gy >= ly) break;
-        T tz[4][1];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const bool ok = z0 + 4 * zh + k < lz;
-          T v;
-          if constexpr (ZZ)
-            v = ok ? ov[y][k] + (T)zz_dec(code[y][k]) : T(0);
-          else
-            v = ok ? (ov[y][k] + (T)code[y][k]) - r : T(0);
-          s[k] = (y > 0) ? v + s[k] : v;
-          tz[k][0] = s[k];
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          hs_step<T, 1, 8, 1>(tz[k], xg);
-          hs_step<T, 1, 8, 2>(tz[k], xg);
-          hs_step<T, 1, 8, 4>(tz[k], xg);
-        }
-        // z Hillis-Steele, d = 1, 2, 4 (descending z keeps each round's sources unmodified);
-        // the upper half reads the lower half's pre-round values
-        {
-          const T l3 = __shfl(tz[3][0], (int)col);  // lower half's t[3] (lane col)
-          tz[3][0] = tz[3][0] + tz[2][0];
-          tz[2][0] = tz[2][0] + tz[1][0];
-          tz[1][0] = tz[1][0] + tz[0][0];
-          if (zh) tz[0][0] = tz[0][0] + l3;
-        }
-        {
-          const T l2 = __shfl(tz[2][0], (int)col), l3 = __shfl(tz[3][0], (int)col);
-          tz[3][0] = tz[3][0] + tz[1][0];
-          tz[2][0] = tz[2][0] + tz[0][0];
-          if (zh) tz[1][0] = tz[1][0] + l3, tz[0][0] = tz[0][0] + l2;
-        }
-        {
-          T lo4[4];
-#pragma unroll
-          for (int k = 0; k < 4; k++) lo4[k] = __shfl(tz[k][0], (int)col);
-          if (zh)
-#pragma unroll
-            for (int k = 0; k < 4; k++) tz[k][0] = tz[k][0] + lo4[k];
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-          if (z0 + 4 * zh + k < lz) out[(size_t)(z0 + 4 * zh + k) * plane + (size_t)gy * lx + xg] = tz[k][0] * ebx2;
+      BPROF(tk = __builtin_readcyclecounter(); pc[3] += tk - tp; tp = tk;)
+      {
+        const uint32_t nyv = min(8u, ly - y0), nzv = min(8u, lz - z0);
+        const size_t base_elem = (size_t)z0 * plane + (size_t)y0 * lx + (size_t)bx * W + (size_t)blk * kBlk;
+        recon_block<T, ZZ, BUF>(tile, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane);
       }
+      hfd::wave_sync();
+      BPROF(tk = __builtin_readcyclecounter(); pc[4] += tk - tp; tp = tk;)
+      // a two-symbol step that crossed the block end left the next block's first symbol in
+      // column 64
+      if (cnt == (uint32_t)(blk + 1) * kBlk + 1u) tile[lane * kTP] = tile[lane * kTP + kBlk];
       hfd::wave_sync();
     }
+    BPROF(tk = __builtin_readcyclecounter(); pc[1] += tk - t0; t0 = tk;)
   }
+#ifdef CUSZ_AMD_DEC_PROFILE
+  pc[6] = wave_sum64(pc[6]);
+  if (lane == 0)
+    for (int i = 0; i < 9; i++) atomicAdd(&g_brick_prof[i], pc[i]);
+#endif
 }
 
 }  // namespace
@@ -587,13 +655,15 @@ BrickGeom brick_geom(int ndim, size_t lx, size_t ly, size_t lz, int elem_bytes)
   return g;
 }
 
+// total LDS (static tables + dynamic per-wave ring and tile) of the fused decoder
 size_t brick_decode_lds(int waves)
 {
   const size_t tab = (sizeof(hfd::LdsTables<kDecB>) + 15) / 16 * 16;
-  return tab + (size_t)waves * ((size_t)kRingRows * 64 + kTileWords) * 4;
+  return tab + (size_t)waves * kDecWaveBytes;
 }
 
-uint32_t brick_decode_max_ahead() { return kRingRows - 6; }
+uint32_t brick_decode_max_ahead() { return kRing - 1; }
+int brick_decode_max_waves() { return kDecMaxWaves; }
 
 int brick_configure(BrickLaunch& L, int elem_bytes, int device)
 {
@@ -672,29 +742,46 @@ int launch_brick_pack(const BrickLaunch& L, const T* in, double eb, int radius, 
 }
 
 template <typename T>
-int launch_brick_decode(const BrickLaunch& L, const uint32_t* bitstream, const uint8_t* revbook, int bklen,
-                        const uint32_t* par_nbit, const uint32_t* par_entry, T* out, double eb, int radius, bool zz,
-                        uint32_t ahead, int waves, unsigned int* work, hipStream_t st)
+int launch_brick_decode(const BrickLaunch& L, const uint32_t* bitstream, size_t bs_words, const uint8_t* revbook,
+                        int bklen, const uint32_t* par_nbit, const uint32_t* par_entry, T* out, double eb, int radius,
+                        bool zz, uint32_t ahead, int waves, unsigned int* work, hipStream_t st)
 {
   const T ebx2 = (T)(eb * 2);  // lrz_x.cuhip.inl:432
   const T r = (T)radius;
   const BrickGeom& g = L.g;
-  const size_t lds = brick_decode_lds(waves);
-  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  if (brick_decode_lds(waves) > 160 * 1024 || waves < 1 || waves > kDecMaxWaves || bs_words >= (1ull << 30))
+    return (int)hipErrorInvalidValue;
+  const size_t lds = (size_t)waves * kDecWaveBytes;  // dynamic part
   const int grid = L.ncu;
-  // diagnostic switch (profiling only): 1 = skip the decode loop, 2 = skip the reconstruction
-  const char* dbs = getenv("CUSZ_AMD_DEC_DEBUG");
-  const int dbg = dbs ? atoi(dbs) : 0;
-  if (zz)
-    k_brick3_decode<T, 4, true><<<grid, 64 * waves, lds, st>>>(bitstream, revbook, bklen, par_nbit, par_entry, out,
-                                                                L.lx, L.ly, L.lz, ebx2, r, g.nbx, g.nby, g.nbricks,
-                                                                ahead, work, dbg);
-  else
-    k_brick3_decode<T, 4, false><<<grid, 64 * waves, lds, st>>>(bitstream, revbook, bklen, par_nbit, par_entry, out,
-                                                                 L.lx, L.ly, L.lz, ebx2, r, g.nbx, g.nby, g.nbricks,
-                                                                 ahead, work, dbg);
+  // buffer stores address a brick block with 32-bit offsets from its first element
+  const size_t plane = (size_t)L.lx * L.ly;
+  const bool buf = (7 * plane + 7 * (size_t)L.lx + (size_t)kBlk) * sizeof(T) < (1ull << 31);
+  const uint32_t bw = (uint32_t)bs_words;
+#define DEC_LAUNCH(ZZ, BUF)                                                                                       \
+  k_brick3_decode<T, ZZ, BUF><<<grid, 64 * waves, lds, st>>>(bitstream, bw, revbook, bklen, par_nbit, par_entry, out, \
+                                                             L.lx, L.ly, L.lz, ebx2, r, g.nbx, g.nby, g.nbricks,      \
+                                                             ahead, work)
+  if (zz) {
+    if (buf) DEC_LAUNCH(true, true); else DEC_LAUNCH(true, false);
+  }
+  else {
+    if (buf) DEC_LAUNCH(false, true); else DEC_LAUNCH(false, false);
+  }
+#undef DEC_LAUNCH
   return (int)hipGetLastError();
 }
+
+#ifdef CUSZ_AMD_DEC_PROFILE
+extern "C" int psz_amd_debug_brick_profile(unsigned long long* host, int reset)
+{
+  hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_brick_prof), sizeof(unsigned long long) * 16);
+  if (reset) {
+    unsigned long long z[16] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_brick_prof), z, sizeof(z));
+  }
+  return (int)e;
+}
+#endif
 
 #define INST(T)                                                                                                   \
   template int launch_brick_scan<T>(const BrickLaunch&, const T*, double, int, bool, const OutlierSink&, uint32_t*, \
@@ -702,9 +789,9 @@ int launch_brick_decode(const BrickLaunch& L, const uint32_t* bitstream, const u
   template int launch_brick_pack<T>(const BrickLaunch&, const T*, double, int, bool, const uint32_t*, int,          \
                                     const uint32_t*, uint32_t*, uint32_t*, uint32_t*, int, unsigned int*,           \
                                     hipStream_t);                                                                  \
-  template int launch_brick_decode<T>(const BrickLaunch&, const uint32_t*, const uint8_t*, int, const uint32_t*,    \
-                                      const uint32_t*, T*, double, int, bool, uint32_t, int, unsigned int*,        \
-                                      hipStream_t);
+  template int launch_brick_decode<T>(const BrickLaunch&, const uint32_t*, size_t, const uint8_t*, int,            \
+                                      const uint32_t*, const uint32_t*, T*, double, int, bool, uint32_t, int,       \
+                                      unsigned int*, hipStream_t);
 INST(float)
 INST(double)
 #undef INST

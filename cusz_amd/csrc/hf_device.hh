@@ -70,12 +70,16 @@ __device__ __forceinline__ void pack_words(uint32_t* cells, uint32_t pos, const 
 }
 
 // ---- decode tables --------------------------------------------------------------------------
-// L1 entry for a B-bit window prefix: [31:30] nsym (1|2, 0 = code longer than B bits),
-// [29:25] bits consumed, [24:20] length of the first code, [19:10] second symbol, [9:0] first.
-__device__ __forceinline__ uint32_t lut_pack(uint32_t nsym, uint32_t bits, uint32_t l0, uint32_t s0, uint32_t s1)
+// Entry (u32) for the codeword(s) at the top of a window: [9:0] first symbol, [25:16] second
+// symbol, [30:26] bits consumed, [31] two symbols.  0 = not in this table.  The symbols sit
+// where one 32-bit LDS store writes them as two consecutive u16 codes (value & 0x03FF03FF).
+__device__ __forceinline__ uint32_t ent_pack(uint32_t two, uint32_t bits, uint32_t s0, uint32_t s1)
 {
-  return (nsym << 30) | (bits << 25) | (l0 << 20) | (s1 << 10) | s0;
+  return (two << 31) | (bits << 26) | (s1 << 16) | s0;
 }
+__device__ __forceinline__ uint32_t ent_bits(uint32_t e) { return (e >> 26) & 31u; }
+__device__ __forceinline__ uint32_t ent_nsym(uint32_t e) { return 1u + (e >> 31); }
+constexpr uint32_t kEntSymMask = 0x03FF03FFu;
 
 // longest code length present (last l with entry[l+1] > entry[l])
 __device__ __forceinline__ int longest_code(const uint32_t* entry)
@@ -101,12 +105,13 @@ __device__ __forceinline__ uint32_t tab_decode1(uint32_t v, const uint32_t* firs
 }
 
 // Decode tables resident in LDS.
-//  L1: 2^B entries indexed by the next B bits, one or two whole codewords of <= B bits.
+//  L1: 2^B entries indexed by the next B bits, one or two whole codewords of <= B bits; 0 for
+//      a prefix of a longer code.
 //  L2: single-symbol entries indexed DIRECTLY by the next 16 bits.  Canonical codes put every
 //      code longer than B bits below first[B] (longer codes are numerically smaller), so only
-//      windows whose B-bit prefix is < first[B] reach it: first[B] << (16 - B) entries (capped;
-//      its last entry stays 0).  L1 and L2 are read together, so a 12..16-bit code costs no
-//      extra round trip.
+//      windows whose B-bit prefix is < first[B] have an entry: first[B] << (16 - B) entries
+//      (capped; its last entry and every entry past them stay 0).  Exactly one of the two
+//      lookups is nonzero for a code of <= 16 bits, so entry = L1 | L2 (read together).
 //  Codes longer than 16 bits (or past the cap) count failing lengths against thresholds the
 //  caller keeps in registers (DecRegs).
 constexpr int kL2Bits = 16;
@@ -159,7 +164,7 @@ __device__ __forceinline__ void build_tables(LdsTables<B>& t, const uint8_t* rev
     if (l0 <= (uint32_t)B) {
       const uint32_t rest = B - l0;
       const uint32_t l1 = rest ? tab_decode1(v << l0, first, maxl, base, t.keys, ub, s1) : 99u;
-      e = l1 <= rest ? lut_pack(2, l0 + l1, l0, s0, s1) : lut_pack(1, l0, l0, s0, 0);
+      e = l1 <= rest ? ent_pack(1, l0 + l1, s0, s1) : ent_pack(0, l0, s0, 0);
     }
     t.l1[i] = e;
   }
@@ -170,7 +175,7 @@ __device__ __forceinline__ void build_tables(LdsTables<B>& t, const uint8_t* rev
     if (q < n2) {
       uint32_t s0;
       const uint32_t l = tab_decode1(q << (32 - kL2Bits), first, maxl, base, t.keys, ub, s0);
-      if (l <= (uint32_t)kL2Bits) e = lut_pack(1, l, l, s0, 0);
+      if (l <= (uint32_t)kL2Bits) e = ent_pack(0, l, s0, 0);
     }
     t.l2[q] = e;
   }
@@ -194,15 +199,15 @@ __device__ __forceinline__ uint32_t lookup(const LdsTables<B>& t, const DecRegs&
 {
   const uint32_t e1 = t.l1[win >> (32 - B)];
   const uint32_t e2 = t.l2[min(win >> (32 - kL2Bits), (uint32_t)kL2Cap - 1)];
-  uint32_t e = (e1 >> 30) ? e1 : e2;
-  if (__builtin_expect(!(e >> 30), 0)) {  // all lengths <= B failed: count the rest
+  uint32_t e = e1 | e2;
+  if (__builtin_expect(e == 0, 0)) {  // all lengths <= 16 failed: count the rest
     uint32_t l = B + 1;
 #pragma unroll
     for (int q = B + 1 - kSlowFrom; q < kLmax - kSlowFrom + 1; q++)
       l += (kSlowFrom + q < (int)rg.maxl && (win >> (32 - (kSlowFrom + q))) < rg.first[q]) ? 1u : 0u;
     if (l > rg.maxl) l = rg.maxl;
     const uint32_t s = t.keys[min(t.base[l] + (win >> (32 - l)), bklen - 1)];
-    e = lut_pack(1, l, l, s, 0);
+    e = ent_pack(0, l, s, 0);
   }
   return e;
 }

@@ -183,6 +183,7 @@ int brick_configure(BrickLaunch& L, int elem_bytes, int device);
 // LDS bytes of the fused decoder for `waves` waves; the largest look-ahead (ring rows) it takes
 size_t brick_decode_lds(int waves);
 uint32_t brick_decode_max_ahead();
+int brick_decode_max_waves();
 
 template <typename T>
 int launch_brick_scan(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const OutlierSink& ol,
@@ -194,9 +195,9 @@ int launch_brick_pack(const BrickLaunch& L, const T* in, double eb, int radius, 
                       int bklen, const uint32_t* bbase, uint32_t* par_nbit, uint32_t* par_entry, uint32_t* bitstream,
                       int reverse, unsigned int* overflow, hipStream_t st);
 template <typename T>
-int launch_brick_decode(const BrickLaunch& L, const uint32_t* bitstream, const uint8_t* revbook, int bklen,
-                        const uint32_t* par_nbit, const uint32_t* par_entry, T* out, double eb, int radius, bool zz,
-                        uint32_t ahead, int waves, unsigned int* work, hipStream_t st);
+int launch_brick_decode(const BrickLaunch& L, const uint32_t* bitstream, size_t bs_words, const uint8_t* revbook,
+                        int bklen, const uint32_t* par_nbit, const uint32_t* par_entry, T* out, double eb, int radius,
+                        bool zz, uint32_t ahead, int waves, unsigned int* work, hipStream_t st);
 
 // min / max (Rel mode, extrema.cuhip.inl:86-208), writes {min, max} as doubles
 template <typename T>

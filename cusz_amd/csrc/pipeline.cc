@@ -556,16 +556,21 @@ struct Pipeline {
     const size_t seg = h->entry[PSZHEADER_ENCODED + 1] - h->entry[PSZHEADER_ENCODED];
     const size_t fixed = 128 + rvbk + 8 * (size_t)pd;
     const size_t cells = seg > fixed ? (seg - fixed) / 4 : 0;
-    // input ring per wave: rows (words of every chunk) issued one 32-symbol block ahead; sized
-    // from the archive's average bits per symbol (a lane that outruns the ring reads HBM)
-    const double words_per_block = (double)cells / std::max<size_t>(pd, 1) * 32.0 / bl.g.W;
-    uint32_t ahead = (uint32_t)(2.4 * words_per_block) + 4;
+    // ring rows prefetched past the fastest lane: about two sub-blocks (32 symbols) of words at
+    // the archive's average bits per symbol
+    const double words_per_sub = (double)cells / std::max<size_t>(pd, 1) * 32.0 / bl.g.W;
+    uint32_t ahead = (uint32_t)(2.5 * words_per_sub) + 3;
     ahead = std::min(ahead, brick_decode_max_ahead());
-    int waves = 12;  // kDecMaxWaves
+    int waves = brick_decode_max_waves();
+    if (const char* w = getenv("CUSZ_AMD_DEC_WAVES")) waves = std::max(1, std::min(waves, atoi(w)));  // TEMP experiment
     while (waves > 1 && brick_decode_lds(waves) > 160 * 1024) waves--;
+    // words from the bitstream start to the end of the archive (range of the decoder's loads)
+    const size_t bits_off = phf_off + 128 + rvbk + 8 * (size_t)pd;
+    const size_t total = h->entry[PSZHEADER_ENC_PASS2_END];
+    const size_t bs_words = total > bits_off ? (total - bits_off) / 4 : 0;
     CUSZ_AMD_HIP_CHECK(hipMemsetAsync(work_counter(), 0, kWorkBytes, stream));
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_decode<T>(
-        bl, reinterpret_cast<const uint32_t*>(phf + 128 + rvbk + 8 * (size_t)pd), phf + 128, bklen,
+        bl, reinterpret_cast<const uint32_t*>(phf + 128 + rvbk + 8 * (size_t)pd), bs_words, phf + 128, bklen,
         reinterpret_cast<const uint32_t*>(phf + 128 + rvbk), reinterpret_cast<const uint32_t*>(phf + 128 + rvbk + 4 * (size_t)pd),
         out, h->rc.eb, h->rc.radius, zz, ahead, waves, work_counter(), stream));
     mark(8);
