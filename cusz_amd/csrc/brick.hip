@@ -24,6 +24,7 @@
 // The archive is the reference phf format: par_entry[c] points at chunk c (the reference decoder
 // reads chunk c from there, hf_kernels.cuhip.inl:386-391); chunks are laid out brick by brick,
 // and the few cells between a brick's last chunk and the next region are zero.
+#include "archive_device.hh"
 #include "common.hh"
 #include "hf_device.hh"
 #include "kernels.hh"
@@ -36,6 +37,12 @@ using namespace lrzd;
 namespace {
 
 constexpr int kBrickWaves = 4;  // waves per workgroup in the encode passes
+#ifndef CUSZ_AMD_HIST_COPIES
+#define CUSZ_AMD_HIST_COPIES 1
+#endif
+constexpr int kHistCopies = CUSZ_AMD_HIST_COPIES;  // lane-interleaved copies of a wave's brick histogram
+// per-brick u16 histograms are stored at a stride of whole 16-B groups (the plan kernel's loads)
+__host__ __device__ constexpr int bhist_stride(int bklen) { return (bklen + 7) & ~7; }
 constexpr int kWorkShards = 8;  // decoder work counters, 64 B apart
 
 __device__ __forceinline__ uint32_t readlane(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
@@ -55,14 +62,21 @@ __device__ __forceinline__ void load_ystep(const T* __restrict__ in, size_t plan
   }
 }
 
+// Prequant of one y-step: p = round(x * ebx2_r) (lrz_c.cuhip.inl:305-309).
 template <typename T, int V>
-__device__ __forceinline__ void predict_ystep(const T (&raw)[8][V], uint32_t x0, int y, T ebx2_r, T (&bprev)[8][V],
-                                              T (&p)[8][V])
+__device__ __forceinline__ void prequant_ystep(const T (&raw)[8][V], T ebx2_r, T (&p)[8][V])
 {
 #pragma unroll
   for (int z = 0; z < 8; z++)
 #pragma unroll
     for (int k = 0; k < V; k++) p[z][k] = dround(raw[z][k] * ebx2_r);
+}
+
+// Residuals of one y-step in place: z-diff, x-diff inside 8-wide tiles (DPP row_shr), y-diff
+// against the previous y-step's z/x residuals (lrz_c.cuhip.inl:341-352 order).
+template <typename T, int V>
+__device__ __forceinline__ void residual_ystep(uint32_t x0, int y, T (&bprev)[8][V], T (&p)[8][V])
+{
 #pragma unroll
   for (int z = 7; z > 0; z--)
 #pragma unroll
@@ -84,66 +98,141 @@ __device__ __forceinline__ void predict_ystep(const T (&raw)[8][V], uint32_t x0,
     }
 }
 
+// The encode passes walk a stream of y-steps: (brick it, y = 0..7), it += waves in the grid.
+// The rows of step s + NB are loaded while step s is computed, across brick boundaries, into the
+// buffer step s has just consumed (NB divides 8, so the fully unrolled y loop needs no copies).
+// NB = 2 for f32 (16 KiB in flight per wave at 2 waves/SIMD); f64 rows are twice as wide: 1.
+template <typename T>
+constexpr int kStepBuffers = sizeof(T) == 4 ? 2 : 1;
+template <typename T, int V>
+struct StepLoader {
+  const T* in;
+  size_t plane;
+  uint32_t lx, ly, lz, nbx, nby, nbricks;
+  int reverse;
+  uint32_t lane;
+  __device__ __forceinline__ uint32_t brick_of(uint32_t it) const { return reverse ? nbricks - 1 - it : it; }
+  // Rows (y, z = 0..7) of brick `it` by raw buffer loads from the brick's origin: one 16-B (f64:
+  // two) load per lane and row, rows outside the field get an offset past the range and read 0.
+  // Straight-line code: no per-row branches, so the waitcnt pass can count the loads exactly.
+  __device__ __forceinline__ void issue(uint32_t it, int y, T (&dst)[8][V]) const
+  {
+    if (it >= nbricks) return;
+    const uint32_t b = brick_of(it), bx = b % nbx, t = b / nbx, by = t % nby, bz = t / nby;
+    const T* origin = in + (size_t)bz * 8 * plane + (size_t)by * 8 * lx + (size_t)bx * (64 * V);
+    const uint32_t span = (uint32_t)(8 * plane * sizeof(T));  // < 2^31 (brick_geom)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(origin), 0, (int)span, 0x00020000);
+    const bool yok = by * 8 + (uint32_t)y < ly;
+    const uint32_t nzv = min(8u, lz - bz * 8);
+#pragma unroll
+    for (int z = 0; z < 8; z++) {
+      const uint32_t off = (yok && (uint32_t)z < nzv)
+                               ? (uint32_t)(((size_t)z * plane + (size_t)y * lx) * sizeof(T)) + lane * (V * sizeof(T))
+                               : span;
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+      for (int h = 0; h < (int)(V * sizeof(T) / 16); h++) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + 16 * h), 0, 0);
+        __builtin_memcpy(reinterpret_cast<char*>(&dst[z][0]) + 16 * h, &v, 16);
+      }
+    }
+  }
+};
+
+template <int V>
+__device__ __forceinline__ void store_codes_row(uint16_t* p, const uint16_t (&q)[V])
+{
+  static_assert(V == 4, "one 8-B store per lane and row");
+  uint2 w;
+  w.x = (uint32_t)q[0] | ((uint32_t)q[1] << 16);
+  w.y = (uint32_t)q[2] | ((uint32_t)q[3] << 16);
+  *reinterpret_cast<uint2*>(p) = w;
+}
+
 // =========================================================================================
 // pass 1: predict -> histograms + outliers
 // =========================================================================================
 template <typename T, int V, bool ZZ>
 __global__ void __launch_bounds__(64 * kBrickWaves)
 k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T ebx2_r, T r, OutlierSink ol,
-              uint32_t* __restrict__ g_hist, uint16_t* __restrict__ bhist, int bklen, uint32_t nbx, uint32_t nby,
-              uint32_t nbricks)
+              uint32_t* __restrict__ g_hist, uint16_t* __restrict__ bhist, uint16_t* __restrict__ bcodes, int bklen,
+              uint32_t nbx, uint32_t nby, uint32_t nbricks)
 {
   extern __shared__ uint32_t smem[];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wid: uniform (SGPR)
   uint32_t* s_wg = smem;                                // workgroup histogram (-> global, once)
-  uint32_t* s_hist = smem + (1 + wid) * kMaxBklen;      // this wave's brick histogram
+  uint32_t* s_hist = smem + (1 + wid * kHistCopies) * kMaxBklen;  // this wave's brick histogram
   for (int i = threadIdx.x; i < bklen; i += blockDim.x) s_wg[i] = 0;
-  for (int i = lane; i < bklen; i += 64) s_hist[i] = 0;
+  for (int i = lane; i < bhist_stride(bklen) * kHistCopies; i += 64) s_hist[i] = 0;
+  const uint32_t hc = (uint32_t)lane & (kHistCopies - 1);
   __syncthreads();
-  const size_t plane = (size_t)lx * ly;
   const uint32_t nw = gridDim.x * kBrickWaves;
-  for (uint32_t brick = blockIdx.x * kBrickWaves + wid; brick < nbricks; brick += nw) {
+  const StepLoader<T, V> ld{in, (size_t)lx * ly, lx, ly, lz, nbx, nby, nbricks, 0, (uint32_t)lane};
+  const size_t plane = ld.plane;
+  uint32_t it = blockIdx.x * kBrickWaves + wid;
+  constexpr int NB = kStepBuffers<T>;
+  T buf[NB][8][V];
+#pragma unroll
+  for (int j = 0; j < NB; j++) ld.issue(it, j, buf[j]);
+  for (; it < nbricks; it += nw) {
+    const uint32_t brick = it;
     const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
     const uint32_t x0 = bx * (64 * V) + lane * V, y0 = by * 8, z0 = bz * 8;
     uint32_t cnt = 0;
-    T bprev[8][V], nxt[8][V];
-    load_ystep<T, V>(in, plane, lx, ly, lz, x0, y0, z0, nxt);
-    for (int y = 0; y < 8; y++) {
+    T bprev[8][V];
+#pragma unroll 1
+    for (int y2 = 0; y2 < 8; y2 += NB)  // not unrolled: instruction cache
+#pragma unroll
+    for (int j = 0; j < NB; j++) {
+      const int y = y2 + j;
+      T d[8][V];
+      prequant_ystep<T, V>(buf[j], ebx2_r, d);
+      if (y + NB < 8) ld.issue(it, y + NB, buf[j]);
+      else ld.issue(it + nw, y + NB - 8, buf[j]);
       const uint32_t gy = y0 + y;
-      if (gy >= ly) break;
-      T raw[8][V], d[8][V];
-#pragma unroll
-      for (int z = 0; z < 8; z++)
-#pragma unroll
-        for (int k = 0; k < V; k++) raw[z][k] = nxt[z][k];
-      if (y < 7) load_ystep<T, V>(in, plane, lx, ly, lz, x0, gy + 1, z0, nxt);
-      predict_ystep<T, V>(raw, x0, y, ebx2_r, bprev, d);
+      if (gy >= ly) continue;
+      residual_ystep<T, V>(x0, y, bprev, d);
+      uint16_t* crow = bcodes + ((size_t)brick * 64 + (size_t)y * 8) * (64 * V) + (size_t)lane * V;
 #pragma unroll
       for (int z = 0; z < 8; z++) {
         if (z0 + z >= lz) break;
         float olv[V];
-        size_t idx[V];
-        uint32_t mask = 0;
-        const size_t base = (size_t)(z0 + z) * plane + (size_t)gy * lx;
+        uint16_t q[V];
+        uint64_t anyol = 0;  // SALU: OR of the per-element outlier lane masks
 #pragma unroll
         for (int k = 0; k < V; k++) {
           bool is_ol;
-          const uint16_t q = quantize<T, ZZ>(d[z][k], r, is_ol, olv[k]);
-          idx[k] = base + x0 + k;
-          atomicAdd(&s_hist[q], 1u);
-          mask |= (uint32_t)is_ol << k;
+          q[k] = quantize<T, ZZ>(d[z][k], r, is_ol, olv[k]);
+          anyol |= __ballot(is_ol);
+#ifndef CUSZ_AMD_DIAG_NOHIST
+          atomicAdd(&s_hist[q[k] * kHistCopies + hc], 1u);
+#else
+          s_hist[q[k] * kHistCopies + hc] = 1u;  // diagnostic: plain store instead of the atomic
+#endif
         }
-        if (__ballot(mask != 0)) emit_outliers<V>(ol, brick, cnt, mask, olv, idx);
+        store_codes_row<V>(crow + (size_t)z * (64 * V), q);
+        if (anyol) {
+          uint32_t mask = 0;
+          size_t idx[V];
+          const size_t base = (size_t)(z0 + z) * plane + (size_t)gy * lx;
+#pragma unroll
+          for (int k = 0; k < V; k++) {
+            mask |= (uint32_t)(q[k] == 0 && (ZZ ? !(dabs(d[z][k]) < r) : true)) << k;
+            idx[k] = base + x0 + k;
+          }
+          emit_outliers<V>(ol, brick, cnt, mask, olv, idx);
+        }
       }
     }
     if (lane == 0) ol.brick_cnt[brick] = cnt;
     hfd::wave_sync();
-    uint16_t* bh = bhist + (size_t)brick * bklen;
-    for (int i = lane; i < bklen; i += 64) {
-      const uint32_t c = s_hist[i];
+    uint16_t* bh = bhist + (size_t)brick * bhist_stride(bklen);
+    for (int i = lane; i < bhist_stride(bklen); i += 64) {
+      uint32_t c = 0;
+#pragma unroll
+      for (int j = 0; j < kHistCopies; j++) c += s_hist[i * kHistCopies + j], s_hist[i * kHistCopies + j] = 0;
       bh[i] = (uint16_t)c;
       if (c) atomicAdd(&s_wg[i], c);
-      s_hist[i] = 0;
     }
     hfd::wave_sync();
   }
@@ -155,74 +244,100 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
 }
 
 // =========================================================================================
-// reservation: per-brick bit count and region size, then the exclusive scan
+// plan: per-brick region sizes and outlier offsets, archive totals and headers
 // =========================================================================================
+// One launch after the codebook upload plans the whole archive:
+//  * per brick: region upper bound ub = (sum_s hist_b[s] len[s] + 31 rows) / 32 cells and its
+//    outlier count; block-local exclusive prefixes of both (kPlanBricks bricks per block);
+//  * block totals by agent-scope atomics; the block that finishes last scans them (every brick's
+//    base = local prefix + block prefix), fills the size fields and writes both headers.
+// Replaces the reference's host-side scans (hf_kernels.cuhip.inl:449-473, compressor.inl:398-418).
+constexpr int kPlanBricks = 64;  // 16 bricks per wave
+
 __device__ __forceinline__ uint32_t brick_rows3(uint32_t brick, uint32_t nbx, uint32_t nby, uint32_t ly, uint32_t lz)
 {
   const uint32_t t = brick / nbx, by = t % nby, bz = t / nby;
   return min(8u, ly - by * 8) * min(8u, lz - bz * 8);
 }
 
-__global__ void __launch_bounds__(256)
-k_brick_reserve(const uint16_t* __restrict__ bhist, int bklen, const uint32_t* __restrict__ book, uint32_t nbricks,
-                uint32_t nbx, uint32_t nby, uint32_t ly, uint32_t lz, uint32_t* __restrict__ ub,
-                unsigned long long* total_nbit)
+__global__ void __launch_bounds__(256) k_brick_plan(BrickPlanArgs a, HeaderTpl tpl)
 {
   __shared__ uint32_t s_len[kMaxBklen];
+  __shared__ uint32_t s_ub[kPlanBricks], s_oc[kPlanBricks];
   __shared__ unsigned long long s_bits[4];
-  for (int i = threadIdx.x; i < bklen; i += 256) s_len[i] = book[i] >> 27;
+  __shared__ uint32_t s_last;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int i = tid; i < a.bhs; i += 256) s_len[i] = i < a.bklen ? a.book[i] >> 27 : 0u;
   __syncthreads();
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const uint32_t brick = blockIdx.x * 4 + wid;
-  uint32_t bits = 0;
-  if (brick < nbricks) {
-    const uint16_t* h = bhist + (size_t)brick * bklen;
-    for (int i = lane; i < bklen; i += 64) bits += (uint32_t)h[i] * s_len[i];
-    bits = hfd::wave_sum(bits);
-    if (lane == 0) ub[brick] = (bits + 31u * brick_rows3(brick, nbx, nby, ly, lz)) >> 5;
+  const uint32_t nblk = gridDim.x, b0 = blockIdx.x * kPlanBricks;
+  unsigned long long wbits = 0;
+  for (int j = 0; j < kPlanBricks / 4; j++) {
+    const uint32_t slot = wid * (kPlanBricks / 4) + j, brick = b0 + slot;
+    uint32_t ub = 0, oc = 0;
+    if (brick < a.nbricks) {
+      const uint16_t* h = a.bhist + (size_t)brick * a.bhs;
+      uint32_t bits = 0;
+      for (int i = lane * 8; i < a.bhs; i += 512) {
+        const uint4 v = *reinterpret_cast<const uint4*>(h + i);  // 8 bins
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) bits += (w[k] & 0xFFFFu) * s_len[i + 2 * k] + (w[k] >> 16) * s_len[i + 2 * k + 1];
+      }
+      bits = hfd::wave_sum(bits);
+      wbits += bits;
+      ub = (bits + 31u * brick_rows3(brick, a.nbx, a.nby, a.ly, a.lz)) >> 5;
+      oc = min(a.brick_cnt[brick], a.cap_per_brick);
+    }
+    if (lane == 0) s_ub[slot] = ub, s_oc[slot] = oc;
   }
-  if (lane == 0) s_bits[wid] = bits;
+  if (lane == 0) s_bits[wid] = wbits;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(total_nbit, s_bits[0] + s_bits[1] + s_bits[2] + s_bits[3]);
-}
-
-// exclusive scan of ub[0..n) into base[0..n]; base[n] = total cells (one workgroup)
-__global__ void __launch_bounds__(1024) k_brick_offsets(const uint32_t* __restrict__ ub, uint32_t n,
-                                                        uint32_t* __restrict__ base, CompressInfo* info)
-{
-  __shared__ uint32_t s_scan[16];
-  __shared__ uint32_t s_carry;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  if (tid == 0) s_carry = 0;
+  if (wid == 0) {  // kPlanBricks == 64: one value per lane
+    const uint32_t ub = s_ub[lane], oc = s_oc[lane];
+    const uint32_t iu = hfd::wave_incl_scan(ub), io = hfd::wave_incl_scan(oc);
+    const uint32_t brick = b0 + lane;
+    if (brick < a.nbricks) a.ub[brick] = ub, a.cell_local[brick] = iu - ub, a.ol_local[brick] = io - oc;
+    if (lane == 63) {
+      atomicExch(a.cell_pre + blockIdx.x, iu);
+      atomicExch(a.ol_pre + blockIdx.x, io);
+      atomicAdd(&a.info->total_nbit, s_bits[0] + s_bits[1] + s_bits[2] + s_bits[3]);
+      const uint32_t ticket =
+          __hip_atomic_fetch_add(&a.info->pad[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = ticket == nblk - 1;
+    }
+  }
   __syncthreads();
-  constexpr int PER = 8;
-  for (uint32_t b0 = 0; b0 < n; b0 += 1024 * PER) {
-    uint32_t v[PER], sum = 0;
-#pragma unroll
-    for (int k = 0; k < PER; k++) {
-      const uint32_t b = b0 + tid * PER + k;
-      v[k] = b < n ? ub[b] : 0u;
-      sum += v[k];
-    }
-    const uint32_t inc = hfd::wave_incl_scan(sum);
-    if (lane == 63) s_scan[wid] = inc;
+  if (!s_last) return;
+  // last block: exclusive scans of the block totals (read back by atomics: other XCDs' L2s)
+  __shared__ uint32_t s_wsum[2][4];
+  __shared__ uint32_t s_carry[2];
+  if (tid < 2) s_carry[tid] = 0;
+  __syncthreads();
+  for (uint32_t c0 = 0; c0 < nblk; c0 += 256) {
+    const uint32_t i = c0 + tid;
+    const uint32_t vc = i < nblk ? atomicAdd(a.cell_pre + i, 0u) : 0u;
+    const uint32_t vo = i < nblk ? atomicAdd(a.ol_pre + i, 0u) : 0u;
+    const uint32_t ic = hfd::wave_incl_scan(vc), io = hfd::wave_incl_scan(vo);
+    if (lane == 63) s_wsum[0][wid] = ic, s_wsum[1][wid] = io;
     __syncthreads();
-    uint32_t off = s_carry;
-    for (int w = 0; w < wid; w++) off += s_scan[w];
-    uint32_t run = off + inc - sum;
-#pragma unroll
-    for (int k = 0; k < PER; k++) {
-      const uint32_t b = b0 + tid * PER + k;
-      if (b < n) base[b] = run;
-      run += v[k];
-    }
+    uint32_t oc = s_carry[0], oo = s_carry[1];
+    for (int w = 0; w < wid; w++) oc += s_wsum[0][w], oo += s_wsum[1][w];
+    if (i < nblk) a.cell_pre[i] = oc + ic - vc, a.ol_pre[i] = oo + io - vo;
     __syncthreads();
-    if (tid == 1023) s_carry = off + inc;
+    if (tid == 255) s_carry[0] = oc + ic, s_carry[1] = oo + io;
     __syncthreads();
   }
   if (tid == 0) {
-    base[n] = s_carry;
-    info->total_ncell = s_carry;
+    const unsigned long long ncell = s_carry[0], slot_total = s_carry[1];
+    a.cell_pre[nblk] = (uint32_t)ncell;
+    a.ol_pre[nblk] = (uint32_t)slot_total;
+    const uint32_t sp = *a.spill_cnt;
+    const uint32_t sp_kept = sp < a.spill_cap ? sp : a.spill_cap;
+    const unsigned long long nbit = __hip_atomic_load(&a.info->total_nbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    a.info->total_ncell = ncell;
+    a.info->splen = slot_total + sp_kept;
+    a.info->outlier_lost = sp > a.spill_cap ? sp - a.spill_cap : 0u;
+    write_headers_dev(a.archive, tpl, nbit, ncell, slot_total + sp_kept, a.phf_offset, a.bitstream_rel);
   }
 }
 
@@ -235,52 +350,72 @@ constexpr int pack_cells_words()
   return ((64 * V * kLmax + 31) / 32 + 4 + 3) / 4 * 4;
 }
 
-template <typename T, int V, bool ZZ>
+// Pass 2 packs the brick's rows from the codes pass 1 left in brick order (row r of brick b at
+// (b * 64 + r) * W): per row, codewords -> wave scan of their lengths -> MSB-first packing into
+// LDS cells (each row starts a new cell, hf_kernels.cuhip.inl:97-157) -> one coalesced copy.
+// The codes of the next y-step are loaded while the current one is packed.
+template <int V>
 __global__ void __launch_bounds__(64 * kBrickWaves)
-k_brick3_pack(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T ebx2_r, T r,
-              const uint32_t* __restrict__ book, int bklen, const uint32_t* __restrict__ bbase,
-              uint32_t* __restrict__ par_nbit, uint32_t* __restrict__ par_entry, uint32_t* __restrict__ bitstream,
-              uint32_t nbx, uint32_t nby, uint32_t nbricks, int reverse, unsigned int* overflow)
+k_brick3_pack(const uint16_t* __restrict__ bcodes, uint32_t ly, uint32_t lz, const uint32_t* __restrict__ book,
+              int bklen, BrickPlanArgs pl, uint32_t* __restrict__ par_nbit, uint32_t* __restrict__ par_entry,
+              uint32_t* __restrict__ bitstream, uint32_t nbx, uint32_t nby, uint32_t nbricks, int reverse,
+              unsigned int* overflow)
 {
+  static_assert(V == 4, "8-B code loads");
   constexpr int CW = pack_cells_words<V>();
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint32_t* s_book = smem;  // kMaxBklen words
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wid: uniform (SGPR)
   uint32_t* cells = smem + kMaxBklen + wid * CW;
   for (int i = threadIdx.x; i < bklen; i += blockDim.x) s_book[i] = book[i];
   for (int i = lane; i < CW; i += 64) cells[i] = 0;
   __syncthreads();
-  const size_t plane = (size_t)lx * ly;
   const uint32_t nw = gridDim.x * kBrickWaves;
+  const uint32_t ncell = pl.cell_pre[pl.nblk];
+  uint2* ol_dst = reinterpret_cast<uint2*>(bitstream + ncell);  // outlier cells follow the bitstream
+  {  // spill list (bricks past their slot; not expected below 10 % outliers) after every slot
+    const uint32_t slot_total = pl.ol_pre[pl.nblk], sp = min(*pl.spill_cnt, pl.spill_cap);
+    for (uint32_t i = (blockIdx.x * kBrickWaves + wid) * 64 + lane; i < sp; i += nw * 64) {
+      const uint64_t c = pl.spill[i];
+      ol_dst[slot_total + i] = make_uint2((uint32_t)c, (uint32_t)(c >> 32));
+    }
+  }
   for (uint32_t it = blockIdx.x * kBrickWaves + wid; it < nbricks; it += nw) {
     const uint32_t brick = reverse ? nbricks - 1 - it : it;
     const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
-    const uint32_t x0 = bx * (64 * V) + lane * V, y0 = by * 8, z0 = bz * 8;
-    const uint32_t base = bbase[brick], lim = bbase[brick + 1] - base;
+    const uint32_t y0 = by * 8, z0 = bz * 8;
+    const uint32_t nyv = min(8u, ly - y0), nzv = min(8u, lz - z0);
+    const uint32_t pb = brick / kPlanBricks;
+    const uint32_t base = pl.cell_local[brick] + pl.cell_pre[pb], lim = pl.ub[brick];
+    {  // this brick's outlier slot -> the archive's outlier segment (brick order)
+      const uint32_t cnt = min(pl.brick_cnt[brick], pl.cap_per_brick);
+      const uint64_t* slot = pl.slots + (size_t)brick * pl.cap_per_brick;
+      uint2* d = ol_dst + pl.ol_local[brick] + pl.ol_pre[pb];
+      for (uint32_t i = lane; i < cnt; i += 64) {
+        const uint64_t c = slot[i];
+        d[i] = make_uint2((uint32_t)c, (uint32_t)(c >> 32));
+      }
+    }
     uint32_t* dst = bitstream + base;
+    const uint2* src = reinterpret_cast<const uint2*>(bcodes + (size_t)brick * 64 * (64 * V)) + lane;
     uint32_t off = 0, my_nbit = 0, my_entry = 0;
-    T bprev[8][V], nxt[8][V];
-    load_ystep<T, V>(in, plane, lx, ly, lz, x0, y0, z0, nxt);
-    for (int y = 0; y < 8; y++) {
-      const uint32_t gy = y0 + y;
-      if (gy >= ly) break;
-      T raw[8][V], d[8][V];
+    uint2 cur[8], nxt[8];
 #pragma unroll
-      for (int z = 0; z < 8; z++)
+    for (int z = 0; z < 8; z++) nxt[z] = (uint32_t)z < nzv ? src[z * 64] : make_uint2(0, 0);
+    for (uint32_t y = 0; y < nyv; y++) {
 #pragma unroll
-        for (int k = 0; k < V; k++) raw[z][k] = nxt[z][k];
-      if (y < 7) load_ystep<T, V>(in, plane, lx, ly, lz, x0, gy + 1, z0, nxt);
-      predict_ystep<T, V>(raw, x0, y, ebx2_r, bprev, d);
+      for (int z = 0; z < 8; z++) cur[z] = nxt[z];
+      if (y + 1 < nyv)
+#pragma unroll
+        for (int z = 0; z < 8; z++) nxt[z] = (uint32_t)z < nzv ? src[((y + 1) * 8 + z) * 64] : make_uint2(0, 0);
 #pragma unroll
       for (int z = 0; z < 8; z++) {
-        if (z0 + z >= lz) break;
+        if ((uint32_t)z >= nzv) break;
+        const uint32_t qs[4] = {cur[z].x & 0xFFFFu, cur[z].x >> 16, cur[z].y & 0xFFFFu, cur[z].y >> 16};
         uint32_t w[V], bits = 0;
 #pragma unroll
         for (int k = 0; k < V; k++) {
-          bool is_ol;
-          float olv;
-          const uint16_t q = quantize<T, ZZ>(d[z][k], r, is_ol, olv);
-          w[k] = s_book[q];
+          w[k] = s_book[qs[k]];
           bits += w[k] >> 27;
         }
         const uint32_t inc = hfd::wave_incl_scan(bits);
@@ -292,7 +427,7 @@ k_brick3_pack(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
           if (off + i < lim) dst[off + i] = cells[i];
           cells[i] = 0;
         }
-        if (lane == y * 8 + z) my_nbit = tot, my_entry = base + off;
+        if ((uint32_t)lane == y * 8 + z) my_nbit = tot, my_entry = base + off;
         off += nc;
         hfd::wave_sync();
       }
@@ -300,7 +435,7 @@ k_brick3_pack(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
     if (off > lim && lane == 0) atomicOr(overflow, 1u);  // cannot happen (region is an upper bound)
     for (uint32_t i = off + lane; i < lim; i += 64) dst[i] = 0u;
     const uint32_t ry = lane >> 3, rz = lane & 7;
-    if (y0 + ry < ly && z0 + rz < lz) {
+    if (ry < nyv && rz < nzv) {
       const size_t c = ((size_t)(z0 + rz) * ly + (y0 + ry)) * nbx + bx;
       par_nbit[c] = my_nbit;
       par_entry[c] = my_entry;
@@ -506,7 +641,7 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
   extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
   hfd::build_tables<kDecB>(tb, revbook, bklen);
   const hfd::DecRegs rg = hfd::load_dec_regs(tb);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wid: uniform (SGPR)
   uint32_t* ring = reinterpret_cast<uint32_t*>(dsm + (size_t)wid * kDecWaveBytes);
   uint16_t* tile = reinterpret_cast<uint16_t*>(ring + kRingWords);
   // logical ring row L lives in slot kRing - (L % kRing); slot 0 repeats the rows L % kRing == 0,
@@ -644,7 +779,8 @@ BrickGeom brick_geom(int ndim, size_t lx, size_t ly, size_t lz, int elem_bytes)
   BrickGeom g{};
   g.V = 4;  // W = 256: f32 16-B loads, f64 32-B loads per lane
   g.W = 64 * g.V;
-  g.ok = ndim == 3 && lx % (size_t)g.W == 0 && lx * ly * lz < (1ull << 32) && (elem_bytes == 4 || elem_bytes == 8);
+  g.ok = ndim == 3 && lx % (size_t)g.W == 0 && lx * ly * lz < (1ull << 32) && (elem_bytes == 4 || elem_bytes == 8) &&
+         8 * lx * ly * (size_t)elem_bytes < (1ull << 31);  // 32-bit buffer offsets within 8 planes
   if (!g.ok) return g;
   g.nbx = (uint32_t)(lx / g.W);
   g.nby = (uint32_t)((ly + 7) / 8);
@@ -671,16 +807,16 @@ int brick_configure(BrickLaunch& L, int elem_bytes, int device)
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1) ncu = 256;
   L.ncu = ncu;
   int per_scan = 0, per_pack = 0;
-  const size_t lds_scan = (size_t)(1 + kBrickWaves) * kMaxBklen * 4;
+  const size_t lds_scan = (size_t)(1 + kBrickWaves * kHistCopies) * kMaxBklen * 4;
   const size_t lds_pack = ((size_t)kMaxBklen + (size_t)kBrickWaves * pack_cells_words<4>()) * 4;
   hipError_t e1, e2;
   if (elem_bytes == 8) {
     e1 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_scan, k_brick3_scan<double, 4, false>, 64 * kBrickWaves, lds_scan);
-    e2 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_pack, k_brick3_pack<double, 4, false>, 64 * kBrickWaves, lds_pack);
+    e2 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_pack, k_brick3_pack<4>, 64 * kBrickWaves, lds_pack);
   }
   else {
     e1 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_scan, k_brick3_scan<float, 4, false>, 64 * kBrickWaves, lds_scan);
-    e2 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_pack, k_brick3_pack<float, 4, false>, 64 * kBrickWaves, lds_pack);
+    e2 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_pack, k_brick3_pack<4>, 64 * kBrickWaves, lds_pack);
   }
   if (e1 != hipSuccess || per_scan < 1) per_scan = 1;
   if (e2 != hipSuccess || per_pack < 1) per_pack = 1;
@@ -694,50 +830,44 @@ int brick_configure(BrickLaunch& L, int elem_bytes, int device)
 
 template <typename T>
 int launch_brick_scan(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const OutlierSink& ol,
-                      uint32_t* hist, uint16_t* bhist, int bklen, hipStream_t st)
+                      uint32_t* hist, uint16_t* bhist, uint16_t* bcodes, int bklen, hipStream_t st)
 {
   const T ebx2_r = (T)(1.0 / (eb * 2));  // lrz_c.cuhip.inl:489
   const T r = (T)radius;
   const BrickGeom& g = L.g;
-  const size_t lds = (size_t)(1 + kBrickWaves) * kMaxBklen * 4;
+  const size_t lds = (size_t)(1 + kBrickWaves * kHistCopies) * kMaxBklen * 4;
   const int grid = L.grid_scan;
   if (zz)
     k_brick3_scan<T, 4, true><<<grid, 64 * kBrickWaves, lds, st>>>(in, L.lx, L.ly, L.lz, ebx2_r, r, ol, hist, bhist,
-                                                                   bklen, g.nbx, g.nby, g.nbricks);
+                                                                   bcodes, bklen, g.nbx, g.nby, g.nbricks);
   else
     k_brick3_scan<T, 4, false><<<grid, 64 * kBrickWaves, lds, st>>>(in, L.lx, L.ly, L.lz, ebx2_r, r, ol, hist, bhist,
-                                                                    bklen, g.nbx, g.nby, g.nbricks);
+                                                                    bcodes, bklen, g.nbx, g.nby, g.nbricks);
   return (int)hipGetLastError();
 }
 
-int launch_brick_reserve(const BrickLaunch& L, const uint16_t* bhist, int bklen, const uint32_t* book, uint32_t* ub,
-                         uint32_t* bbase, CompressInfo* info, hipStream_t st)
+int launch_brick_plan(const BrickLaunch& L, const BrickPlanArgs& a, const void* psz_tpl, const void* phf_tpl,
+                      hipStream_t st)
 {
-  const BrickGeom& g = L.g;
-  k_brick_reserve<<<(g.nbricks + 3) / 4, 256, 0, st>>>(bhist, bklen, book, g.nbricks, g.nbx, g.nby, L.ly, L.lz, ub,
-                                                       &info->total_nbit);
-  k_brick_offsets<<<1, 1024, 0, st>>>(ub, g.nbricks, bbase, info);
+  HeaderTpl t;
+  __builtin_memcpy(t.psz, psz_tpl, 176);
+  __builtin_memcpy(t.phf, phf_tpl, 64);
+  k_brick_plan<<<a.nblk, 256, 0, st>>>(a, t);
   return (int)hipGetLastError();
 }
 
-template <typename T>
-int launch_brick_pack(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const uint32_t* book,
-                      int bklen, const uint32_t* bbase, uint32_t* par_nbit, uint32_t* par_entry, uint32_t* bitstream,
+uint32_t brick_plan_blocks(uint32_t nbricks) { return (nbricks + kPlanBricks - 1) / kPlanBricks; }
+int brick_hist_stride(int bklen) { return bhist_stride(bklen); }
+
+int launch_brick_pack(const BrickLaunch& L, const uint16_t* bcodes, const uint32_t* book, int bklen,
+                      const BrickPlanArgs& plan, uint32_t* par_nbit, uint32_t* par_entry, uint32_t* bitstream,
                       int reverse, unsigned int* overflow, hipStream_t st)
 {
-  const T ebx2_r = (T)(1.0 / (eb * 2));
-  const T r = (T)radius;
   const BrickGeom& g = L.g;
   const size_t lds = ((size_t)kMaxBklen + (size_t)kBrickWaves * pack_cells_words<4>()) * 4;
-  const int grid = L.grid_pack;
-  if (zz)
-    k_brick3_pack<T, 4, true><<<grid, 64 * kBrickWaves, lds, st>>>(in, L.lx, L.ly, L.lz, ebx2_r, r, book, bklen, bbase,
-                                                                   par_nbit, par_entry, bitstream, g.nbx, g.nby,
-                                                                   g.nbricks, reverse, overflow);
-  else
-    k_brick3_pack<T, 4, false><<<grid, 64 * kBrickWaves, lds, st>>>(in, L.lx, L.ly, L.lz, ebx2_r, r, book, bklen,
-                                                                    bbase, par_nbit, par_entry, bitstream, g.nbx,
-                                                                    g.nby, g.nbricks, reverse, overflow);
+  k_brick3_pack<4><<<L.grid_pack, 64 * kBrickWaves, lds, st>>>(bcodes, L.ly, L.lz, book, bklen, plan, par_nbit,
+                                                               par_entry, bitstream, g.nbx, g.nby, g.nbricks, reverse,
+                                                               overflow);
   return (int)hipGetLastError();
 }
 
@@ -785,10 +915,7 @@ extern "C" int psz_amd_debug_brick_profile(unsigned long long* host, int reset)
 
 #define INST(T)                                                                                                   \
   template int launch_brick_scan<T>(const BrickLaunch&, const T*, double, int, bool, const OutlierSink&, uint32_t*, \
-                                    uint16_t*, int, hipStream_t);                                                  \
-  template int launch_brick_pack<T>(const BrickLaunch&, const T*, double, int, bool, const uint32_t*, int,          \
-                                    const uint32_t*, uint32_t*, uint32_t*, uint32_t*, int, unsigned int*,           \
-                                    hipStream_t);                                                                  \
+                                    uint16_t*, uint16_t*, int, hipStream_t);                                       \
   template int launch_brick_decode<T>(const BrickLaunch&, const uint32_t*, size_t, const uint8_t*, int,            \
                                       const uint32_t*, const uint32_t*, T*, double, int, bool, uint32_t, int,       \
                                       unsigned int*, hipStream_t);

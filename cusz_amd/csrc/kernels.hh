@@ -185,14 +185,40 @@ size_t brick_decode_lds(int waves);
 uint32_t brick_decode_max_ahead();
 int brick_decode_max_waves();
 
+// pass 1: predict -> global + per-brick histograms, outliers, codes in brick order (bcodes:
+// nbricks * 64 rows * W u16)
 template <typename T>
 int launch_brick_scan(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const OutlierSink& ol,
-                      uint32_t* hist, uint16_t* bhist, int bklen, hipStream_t st);
-int launch_brick_reserve(const BrickLaunch& L, const uint16_t* bhist, int bklen, const uint32_t* book, uint32_t* ub,
-                         uint32_t* bbase, CompressInfo* info, hipStream_t st);
-template <typename T>
-int launch_brick_pack(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const uint32_t* book,
-                      int bklen, const uint32_t* bbase, uint32_t* par_nbit, uint32_t* par_entry, uint32_t* bitstream,
+                      uint32_t* hist, uint16_t* bhist, uint16_t* bcodes, int bklen, hipStream_t st);
+// archive plan (brick.hip k_brick_plan): region sizes, cell / outlier offsets, totals, headers
+struct BrickPlanArgs {
+  const uint16_t* bhist;  // per-brick histograms, stride brick_hist_stride(bklen)
+  int bklen, bhs;
+  const uint32_t* book;
+  uint32_t nbricks, nbx, nby, ly, lz;
+  const uint32_t* brick_cnt;  // outliers per brick (pass 1)
+  uint32_t cap_per_brick;
+  const uint64_t* slots;      // per-brick outlier slots
+  const uint64_t* spill;
+  const uint32_t* spill_cnt;
+  uint32_t spill_cap;
+  uint32_t nblk;              // plan blocks = brick_plan_blocks(nbricks)
+  uint32_t* ub;               // per brick: region cells
+  uint32_t* cell_local;       // per brick: cell offset inside its plan block
+  uint32_t* ol_local;         // per brick: outlier offset inside its plan block
+  uint32_t* cell_pre;         // nblk + 1: block prefixes, [nblk] = total cells
+  uint32_t* ol_pre;           // nblk + 1: block prefixes, [nblk] = slot outliers
+  CompressInfo* info;         // totals; info->pad[0] = block ticket (zeroed per call)
+  uint8_t* archive;
+  size_t phf_offset, bitstream_rel;
+};
+uint32_t brick_plan_blocks(uint32_t nbricks);
+int brick_hist_stride(int bklen);
+int launch_brick_plan(const BrickLaunch& L, const BrickPlanArgs& a, const void* psz_tpl, const void* phf_tpl,
+                      hipStream_t st);
+// pass 2: brick-ordered codes -> Huffman cells at each brick's reserved region
+int launch_brick_pack(const BrickLaunch& L, const uint16_t* bcodes, const uint32_t* book, int bklen,
+                      const BrickPlanArgs& plan, uint32_t* par_nbit, uint32_t* par_entry, uint32_t* bitstream,
                       int reverse, unsigned int* overflow, hipStream_t st);
 template <typename T>
 int launch_brick_decode(const BrickLaunch& L, const uint32_t* bitstream, size_t bs_words, const uint8_t* revbook,

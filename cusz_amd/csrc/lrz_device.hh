@@ -206,17 +206,13 @@ __device__ __forceinline__ uint16_t quantize(T d, T r, bool& ol, float& olval)
   }
 }
 
-// Emit the outliers of one wave row in (lane, k) order into the brick's slot.
+// Rare path of emit_outliers: some cells of this row go past the brick's slot (out of line:
+// it must not bloat the unrolled hot loops).
 template <int V>
-__device__ __forceinline__ void emit_outliers(const OutlierSink& ol, uint32_t brick, uint32_t& cnt,
-                                              uint32_t mask, const float (&val)[V],
-                                              const size_t (&idx)[V])
+__device__ __forceinline__ void emit_outliers_spill(const OutlierSink& ol, uint32_t brick, uint32_t pos,
+                                                              uint32_t mask, const float (&val)[V],
+                                                              const size_t (&idx)[V])
 {
-  const int c = __popc(mask);
-  const uint64_t b0 = __ballot(c & 1), b1 = __ballot(c & 2), b2 = __ballot(c & 4);
-  const uint64_t lt = lanemask_lt();
-  uint32_t pos = cnt + __popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt);
-  const uint32_t tot = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
   uint64_t* slot = ol.slots + (size_t)brick * ol.cap_per_brick;
 #pragma unroll
   for (int k = 0; k < V; k++) {
@@ -231,6 +227,27 @@ __device__ __forceinline__ void emit_outliers(const OutlierSink& ol, uint32_t br
       pos++;
     }
   }
+}
+
+// Emit the outliers of one wave row in (lane, k) order into the brick's slot.
+template <int V>
+__device__ __forceinline__ void emit_outliers(const OutlierSink& ol, uint32_t brick, uint32_t& cnt,
+                                              uint32_t mask, const float (&val)[V],
+                                              const size_t (&idx)[V])
+{
+  const int c = __popc(mask);
+  const uint64_t b0 = __ballot(c & 1), b1 = __ballot(c & 2), b2 = __ballot(c & 4);
+  const uint64_t lt = lanemask_lt();
+  uint32_t pos = cnt + __popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt);
+  const uint32_t tot = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+  if (__builtin_expect(cnt + tot <= ol.cap_per_brick, 1)) {  // uniform: the whole row fits the slot
+    uint64_t* slot = ol.slots + (size_t)brick * ol.cap_per_brick;
+#pragma unroll
+    for (int k = 0; k < V; k++)
+      if ((mask >> k) & 1u) slot[pos++] = make_cell(val[k], (uint32_t)idx[k]);
+  }
+  else
+    emit_outliers_spill<V>(ol, brick, pos, mask, val, idx);
   cnt += tot;
 }
 

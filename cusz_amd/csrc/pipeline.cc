@@ -81,7 +81,8 @@ struct Pipeline {
   int layout = 0;                 // PSZ_AMD_LAYOUT_*: 0 brick layout when eligible, 1 reference layout
   uint16_t* d_bhist = nullptr;    // per-brick u16 histograms (pass 1 -> reservation)
   uint32_t* d_ub = nullptr;       // per-brick region upper bounds (cells)
-  uint32_t* d_bbase = nullptr;    // exclusive scan of d_ub, nbricks + 1
+  uint32_t* d_bbase = nullptr;    // per-brick cell offsets inside their plan block
+  uint32_t* d_plan = nullptr;     // plan block prefixes: cells | outliers (nblk + 1 each)
   SplineGeom sgeom{};
   uint32_t spl_cap = 0;           // outlier slots per spline tile
   size_t spl_slot_cells = 0;      // capacity of the spline slot area (allocated on first use)
@@ -144,7 +145,7 @@ struct Pipeline {
     for (void* p : {(void*)d_codes, (void*)d_hist, (void*)d_book, (void*)d_slots, (void*)d_brick_cnt,
                     (void*)d_brick_off, (void*)d_spill, (void*)d_small, (void*)d_status, (void*)d_archive,
                     (void*)d_enc_temp, (void*)d_spl_slots, (void*)d_spl_cnt, (void*)d_spl_off, (void*)d_spl_x, (void*)d_spl_sps,
-                    (void*)d_bhist, (void*)d_ub, (void*)d_bbase})
+                    (void*)d_bhist, (void*)d_ub, (void*)d_bbase, (void*)d_plan})
       if (p) (void)hipFree(p);
     if (h_xfer) (void)hipHostFree(h_xfer);
     for (auto& e : ev)
@@ -152,7 +153,7 @@ struct Pipeline {
     d_codes = nullptr, d_hist = nullptr, d_book = nullptr, d_slots = nullptr, d_brick_cnt = nullptr;
     d_brick_off = nullptr, d_spill = nullptr, d_small = nullptr, d_status = nullptr, d_archive = nullptr;
     d_enc_temp = nullptr;
-    d_bhist = nullptr, d_ub = nullptr, d_bbase = nullptr;
+    d_bhist = nullptr, d_ub = nullptr, d_bbase = nullptr, d_plan = nullptr;
     d_spl_slots = nullptr, d_spl_cnt = nullptr, d_spl_off = nullptr, d_spl_x = nullptr, d_spl_sps = nullptr;
     spl_slot_cells = 0, spl_x_words = 0;
     h_xfer = nullptr;
@@ -201,9 +202,12 @@ struct Pipeline {
       CUSZ_AMD_HIP_CHECK(hipMalloc(&d_bhist, (size_t)bl.g.nbricks * kMaxBklen * sizeof(uint16_t)));
       CUSZ_AMD_HIP_CHECK(hipMalloc(&d_ub, (size_t)bl.g.nbricks * 4));
       CUSZ_AMD_HIP_CHECK(hipMalloc(&d_bbase, ((size_t)bl.g.nbricks + 1) * 4));
+      CUSZ_AMD_HIP_CHECK(hipMalloc(&d_plan, 2 * ((size_t)brick_plan_blocks(bl.g.nbricks) + 1) * 4));
     }
 
-    CUSZ_AMD_HIP_CHECK(hipMalloc(&d_codes, (n + 64) * sizeof(uint16_t)));
+    // codes: index order (reference layout) or brick order (brick layout: whole bricks)
+    const size_t code_len = std::max(n + 64, bl.g.ok ? (size_t)bl.g.nbricks * bl.g.brick_elems : 0);
+    CUSZ_AMD_HIP_CHECK(hipMalloc(&d_codes, code_len * sizeof(uint16_t)));
     CUSZ_AMD_HIP_CHECK(hipMalloc(&d_hist, kMaxBklen * sizeof(uint32_t)));
     CUSZ_AMD_HIP_CHECK(hipMalloc(&d_book, kMaxBklen * sizeof(uint32_t)));
     CUSZ_AMD_HIP_CHECK(hipMalloc(&d_slots, slot_cells * 8));
@@ -417,7 +421,8 @@ struct Pipeline {
     const int bsub = g.W, bpar = (int)g.nchunks;
     const uint32_t cap = brick_cap();
     OutlierSink ol{d_slots, d_brick_cnt, d_spill, spill_cnt(), cap, spill_cap, nullptr};
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_scan<T>(bl, in, eb, radius, zz, ol, d_hist, d_bhist, bklen, stream));
+    CUSZ_AMD_HIP_CHECK(
+        (hipError_t)launch_brick_scan<T>(bl, in, eb, radius, zz, ol, d_hist, d_bhist, d_codes, bklen, stream));
     mark(2);
 
     int fs = fetch(regions({{h_hist(), d_hist, (size_t)bklen * 4}}), 2);
@@ -434,18 +439,8 @@ struct Pipeline {
     uint32_t* par_nbit = reinterpret_cast<uint32_t*>(d_archive + phf_off + nbit_rel);
     uint32_t* par_entry = reinterpret_cast<uint32_t*>(d_archive + phf_off + entry_rel);
     uint32_t* bits = reinterpret_cast<uint32_t*>(d_archive + phf_off + bits_rel);
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_reserve(bl, d_bhist, bklen, d_book, d_ub, d_bbase, info(), stream));
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_pack<T>(bl, in, eb, radius, zz, d_book, bklen, d_bbase, par_nbit,
-                                                         par_entry, bits, pack_reverse, timeout(), stream));
-    mark(4);
 
-    FinalizeArgs fa{par_nbit, par_entry, bpar, d_brick_cnt, g.nbricks, cap, spill_cnt(), spill_cap, d_brick_off,
-                    info(), nullptr, true};
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_finalize_scan(fa, stream));
-    OutlierCopyArgs oa{d_slots, d_brick_cnt, d_brick_off, g.nbricks, cap, d_spill, spill_cnt(), spill_cap,
-                       info(), d_archive, phf_off + bits_rel, nullptr};
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_outlier_copy(oa, stream));
-
+    // header templates: static fields from the host, sizes filled by the plan kernel
     h->vle_sublen = bsub;
     h->vle_pardeg = bpar;
     h->len = len;
@@ -455,7 +450,15 @@ struct Pipeline {
     ph.bklen = bklen, ph.sublen = bsub, ph.pardeg = bpar, ph.original_len = n;
     ph.entry[0] = 0, ph.entry[1] = 128, ph.entry[2] = (uint32_t)nbit_rel, ph.entry[3] = (uint32_t)entry_rel;
     ph.entry[4] = (uint32_t)bits_rel;
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_write_headers(d_archive, h, &ph, info(), phf_off, bits_rel, stream));
+
+    const uint32_t nblk = brick_plan_blocks(g.nbricks);
+    BrickPlanArgs pa{d_bhist, bklen, brick_hist_stride(bklen), d_book, g.nbricks, g.nbx, g.nby, bl.ly, bl.lz,
+                     d_brick_cnt, cap, d_slots, d_spill, spill_cnt(), spill_cap, nblk, d_ub, d_bbase, d_brick_off,
+                     d_plan, d_plan + nblk + 1, info(), d_archive, phf_off, bits_rel};
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_plan(bl, pa, h, &ph, stream));
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_pack(bl, d_codes, d_book, bklen, pa, par_nbit, par_entry, bits,
+                                                     pack_reverse, timeout(), stream));
+    mark(4);
     mark(5);
     return finish_compress(h, out, outlen);
   }
@@ -483,6 +486,9 @@ struct Pipeline {
       stage_ms[PSZ_AMD_T_FINALIZE] = span(4, 5);
       stage_ms[PSZ_AMD_T_COMPRESS] = span(0, 5);
     }
+#ifdef CUSZ_AMD_DIAG_NOHIST  // diagnostic build: the reservation is knowingly wrong
+    tmo = 0;
+#endif
     if (tmo) {
       std::fprintf(stderr, "[cusz_amd] encoder reservation/look-back check failed\n");
       return PSZ_ABORT_NOT_IMPLEMENTED;

@@ -5,6 +5,7 @@
 // Reference counterparts: compress wrap-up psz/src/compressor.inl:398-418 (D2D concat),
 // phf header/offsets codec/hf/src/hf_buf.cc:191-211, GPU_extrema
 // psz/src/stat/detail/extrema.cuhip.inl:86-208.
+#include "archive_device.hh"
 #include "common.hh"
 #include "kernels.hh"
 
@@ -126,34 +127,11 @@ __global__ void __launch_bounds__(256) k_outlier_copy(OutlierCopyArgs a, uint32_
   }
 }
 
-struct HeaderTpl {
-  uint32_t psz[176 / 4];
-  uint32_t phf[64 / 4];
-};
-
 __global__ void k_write_headers(uint8_t* archive, HeaderTpl t, const CompressInfo* info, size_t phf_offset,
                                 size_t bitstream_rel)
 {
-  if (threadIdx.x != 0) return;
-  // phf header (hf.h:40-46): total_nbit @24, total_ncell @32, entry[6] @40
-  uint32_t* phf = t.phf;
-  const unsigned long long nb = info->total_nbit, nc = info->total_ncell, sp = info->splen;
-  phf[6] = (uint32_t)nb, phf[7] = (uint32_t)(nb >> 32);
-  phf[8] = (uint32_t)nc, phf[9] = (uint32_t)(nc >> 32);
-  const uint32_t phf_end = (uint32_t)(bitstream_rel + nc * 4);
-  phf[10 + 5] = phf_end;  // entry[END]; entries 0..4 are static, set by the host
-  // psz header (header.h:19-48): entry[6] @56, splen @104
-  uint32_t* psz = t.psz;
-  const uint32_t e_spfmt = (uint32_t)(phf_offset + phf_end);
-  psz[14 + 3] = e_spfmt;
-  psz[14 + 4] = (uint32_t)(e_spfmt + sp * 8);
-  psz[14 + 5] = (uint32_t)(e_spfmt + sp * 8);
-  psz[26] = (uint32_t)sp, psz[27] = (uint32_t)(sp >> 32);
-  uint32_t* a32 = reinterpret_cast<uint32_t*>(archive);
-  for (int i = 0; i < 176 / 4; i++) a32[i] = psz[i];
-  uint32_t* p32 = reinterpret_cast<uint32_t*>(archive + phf_offset);
-  for (int i = 0; i < 64 / 4; i++) p32[i] = phf[i];
-  for (int i = 64 / 4; i < 128 / 4; i++) p32[i] = 0;  // defined padding (reference: stale)
+  if (threadIdx.x == 0)
+    write_headers_dev(archive, t, info->total_nbit, info->total_ncell, info->splen, phf_offset, bitstream_rel);
 }
 
 template <typename T>
