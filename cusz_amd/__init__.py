@@ -99,6 +99,8 @@ EXPORTS = [
     # cusz_amd.h
     "psz_amd_get_internals", "psz_amd_enable_timing", "psz_amd_stage_times", "psz_amd_set_sublen",
     "psz_amd_decode_codes", "psz_amd_set_decoder", "psz_amd_set_layout", "psz_amd_version",
+    "psz_amd_compress_scan_float", "psz_amd_compress_scan_double", "psz_amd_compress_finish",
+    "psz_amd_merge_archives",
 ]
 
 
@@ -141,6 +143,16 @@ def lib():
     L.psz_amd_set_decoder.argtypes = [P, C.c_int]
     L.psz_amd_set_layout.argtypes = [P, C.c_int]
     L.psz_amd_version.restype = C.c_char_p
+    for fn in (L.psz_amd_compress_scan_float, L.psz_amd_compress_scan_double):
+        fn.restype = C.c_int
+        fn.argtypes = [P, psz_rc2, P, P]
+    L.psz_amd_compress_finish.restype = C.c_int
+    L.psz_amd_compress_finish.argtypes = [P, P, C.POINTER(psz_header), C.POINTER(C.c_void_p),
+                                          C.POINTER(C.c_size_t)]
+    L.psz_amd_merge_archives.restype = C.c_int
+    L.psz_amd_merge_archives.argtypes = [C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.c_int,
+                                         C.POINTER(C.c_size_t), psz_len, P, C.c_size_t,
+                                         C.POINTER(C.c_size_t)]
     L.phf_coarse_tune.argtypes = [C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.pszheader_filesize.restype = C.c_size_t
     L.pszheader_filesize.argtypes = [C.POINTER(psz_header)]
@@ -200,6 +212,24 @@ class Resource:
             raise PszError(st, "psz_compress")
         return out.value, nbytes.value, st
 
+    def compress_scan(self, d_in: int, eb: float, d_hist: int, mode: int = Abs, radius: int = 512):
+        """Pass 1 of a sharded compress: the slab's histogram u32[2 radius] goes to d_hist."""
+        f = lib().psz_amd_compress_scan_float if self.dtype == F4 else lib().psz_amd_compress_scan_double
+        st = f(self._h, psz_rc2(mode, eb, radius), C.c_void_p(d_in), C.c_void_p(d_hist))
+        if st not in (PSZ_SUCCESS, PSZ_WARN_RADIUS_TOO_LARGE):
+            raise PszError(st, "psz_amd_compress_scan")
+        return st
+
+    def compress_finish(self, d_hist: int = 0):
+        """Codebook from the device histogram d_hist (0: the slab's own) -> archive."""
+        out = C.c_void_p()
+        nbytes = C.c_size_t()
+        st = lib().psz_amd_compress_finish(self._h, C.c_void_p(d_hist or None), C.byref(self.header),
+                                           C.byref(out), C.byref(nbytes))
+        if st != PSZ_SUCCESS:
+            raise PszError(st, "psz_amd_compress_finish")
+        return out.value, nbytes.value, st
+
     def decompress(self, d_archive: int, nbytes: int, d_out: int):
         L = lib()
         f = L.psz_decompress_float if self.dtype == F4 else L.psz_decompress_double
@@ -257,6 +287,26 @@ def hip_memcpy(dst: int, src: int, nbytes: int, kind: int) -> None:
     st = _hip.hipMemcpy(C.c_void_p(dst), C.c_void_p(src), nbytes, kind)
     if st != 0:
         raise RuntimeError(f"hipMemcpy failed: {st}")
+
+
+def merge_archives(parts, full_dims, offsets=None) -> bytes:
+    """psz_amd_merge_archives over host byte strings (field order) -> the merged archive."""
+    L = lib()
+    bufs = [C.create_string_buffer(bytes(p), len(p)) for p in parts]
+    ptrs = (C.c_void_p * len(parts))(*[C.cast(b, C.c_void_p) for b in bufs])
+    sizes = (C.c_size_t * len(parts))(*[len(p) for p in parts])
+    offs = (C.c_size_t * len(parts))(*offsets) if offsets is not None else None
+    x, y, z = (tuple(full_dims) + (1, 1, 1))[:3]
+    need = C.c_size_t()
+    L.psz_amd_merge_archives(ptrs, sizes, len(parts), offs, psz_len(x, y, z), None, 0, C.byref(need))
+    if need.value == 0:
+        raise PszError(5, "psz_amd_merge_archives")
+    out = C.create_string_buffer(need.value)
+    st = L.psz_amd_merge_archives(ptrs, sizes, len(parts), offs, psz_len(x, y, z), out, need.value,
+                                  C.byref(need))
+    if st != PSZ_SUCCESS:
+        raise PszError(st, "psz_amd_merge_archives")
+    return out.raw[: need.value]
 
 
 def coarse_tune(n: int):

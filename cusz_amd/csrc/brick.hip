@@ -37,6 +37,10 @@ using namespace lrzd;
 namespace {
 
 constexpr int kBrickWaves = 4;  // waves per workgroup in the encode passes
+// A unit = kUnitBricks consecutive bricks, processed by one wave in both encode passes: one
+// histogram record (u16 counts: a unit has at most 32768 elements), one outlier slot and one
+// reserved bitstream region per unit.
+constexpr int kUnitBricks = 1;
 #ifndef CUSZ_AMD_HIST_COPIES
 #define CUSZ_AMD_HIST_COPIES 1
 #endif
@@ -169,70 +173,81 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
   const uint32_t nw = gridDim.x * kBrickWaves;
   const StepLoader<T, V> ld{in, (size_t)lx * ly, lx, ly, lz, nbx, nby, nbricks, 0, (uint32_t)lane};
   const size_t plane = ld.plane;
-  uint32_t it = blockIdx.x * kBrickWaves + wid;
+  const uint32_t nunits = (nbricks + kUnitBricks - 1) / kUnitBricks;
+  const int hs = bhist_stride(bklen);
+  uint32_t u = blockIdx.x * kBrickWaves + wid;
   constexpr int NB = kStepBuffers<T>;
   T buf[NB][8][V];
 #pragma unroll
-  for (int j = 0; j < NB; j++) ld.issue(it, j, buf[j]);
-  for (; it < nbricks; it += nw) {
-    const uint32_t brick = it;
-    const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
-    const uint32_t x0 = bx * (64 * V) + lane * V, y0 = by * 8, z0 = bz * 8;
+  for (int j = 0; j < NB; j++) ld.issue(u * kUnitBricks, j, buf[j]);
+  for (; u < nunits; u += nw) {
     uint32_t cnt = 0;
-    T bprev[8][V];
+    const uint32_t bend = min((u + 1) * kUnitBricks, nbricks);
+    for (uint32_t brick = u * kUnitBricks; brick < bend; brick++) {
+      const uint32_t bnext = brick + 1 < bend ? brick + 1 : (u + nw) * kUnitBricks;  // next brick of the stream
+      const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
+      const uint32_t x0 = bx * (64 * V) + lane * V, y0 = by * 8, z0 = bz * 8;
+      T bprev[8][V];
 #pragma unroll 1
-    for (int y2 = 0; y2 < 8; y2 += NB)  // not unrolled: instruction cache
+      for (int y2 = 0; y2 < 8; y2 += NB)  // not unrolled: instruction cache
 #pragma unroll
-    for (int j = 0; j < NB; j++) {
-      const int y = y2 + j;
-      T d[8][V];
-      prequant_ystep<T, V>(buf[j], ebx2_r, d);
-      if (y + NB < 8) ld.issue(it, y + NB, buf[j]);
-      else ld.issue(it + nw, y + NB - 8, buf[j]);
-      const uint32_t gy = y0 + y;
-      if (gy >= ly) continue;
-      residual_ystep<T, V>(x0, y, bprev, d);
-      uint16_t* crow = bcodes + ((size_t)brick * 64 + (size_t)y * 8) * (64 * V) + (size_t)lane * V;
+        for (int j = 0; j < NB; j++) {
+          const int y = y2 + j;
+          T d[8][V];
+          prequant_ystep<T, V>(buf[j], ebx2_r, d);
+          if (y + NB < 8) ld.issue(brick, y + NB, buf[j]);
+          else ld.issue(bnext, y + NB - 8, buf[j]);
+          const uint32_t gy = y0 + y;
+          if (gy >= ly) continue;
+          residual_ystep<T, V>(x0, y, bprev, d);
+          uint16_t* crow = bcodes + ((size_t)brick * 64 + (size_t)y * 8) * (64 * V) + (size_t)lane * V;
 #pragma unroll
-      for (int z = 0; z < 8; z++) {
-        if (z0 + z >= lz) break;
-        float olv[V];
-        uint16_t q[V];
-        uint64_t anyol = 0;  // SALU: OR of the per-element outlier lane masks
+          for (int z = 0; z < 8; z++) {
+            if (z0 + z >= lz) break;
+            float olv[V];
+            uint16_t q[V];
+            uint64_t anyol = 0;  // SALU: OR of the per-element outlier lane masks
 #pragma unroll
-        for (int k = 0; k < V; k++) {
-          bool is_ol;
-          q[k] = quantize<T, ZZ>(d[z][k], r, is_ol, olv[k]);
-          anyol |= __ballot(is_ol);
-#ifndef CUSZ_AMD_DIAG_NOHIST
-          atomicAdd(&s_hist[q[k] * kHistCopies + hc], 1u);
-#else
-          s_hist[q[k] * kHistCopies + hc] = 1u;  // diagnostic: plain store instead of the atomic
-#endif
-        }
-        store_codes_row<V>(crow + (size_t)z * (64 * V), q);
-        if (anyol) {
-          uint32_t mask = 0;
-          size_t idx[V];
-          const size_t base = (size_t)(z0 + z) * plane + (size_t)gy * lx;
+            for (int k = 0; k < V; k++) {
+              bool is_ol;
+              q[k] = quantize<T, ZZ>(d[z][k], r, is_ol, olv[k]);
+              anyol |= __ballot(is_ol);
+              atomicAdd(&s_hist[q[k] * kHistCopies + hc], 1u);
+            }
+            store_codes_row<V>(crow + (size_t)z * (64 * V), q);
+            if (anyol) {
+              uint32_t mask = 0;
+              size_t idx[V];
+              const size_t base = (size_t)(z0 + z) * plane + (size_t)gy * lx;
 #pragma unroll
-          for (int k = 0; k < V; k++) {
-            mask |= (uint32_t)(q[k] == 0 && (ZZ ? !(dabs(d[z][k]) < r) : true)) << k;
-            idx[k] = base + x0 + k;
+              for (int k = 0; k < V; k++) {
+                mask |= (uint32_t)(q[k] == 0 && (ZZ ? !(dabs(d[z][k]) < r) : true)) << k;
+                idx[k] = base + x0 + k;
+              }
+              emit_outliers<V>(ol, u, cnt, mask, olv, idx);  // one slot per unit
+            }
           }
-          emit_outliers<V>(ol, brick, cnt, mask, olv, idx);
         }
-      }
     }
-    if (lane == 0) ol.brick_cnt[brick] = cnt;
+    if (lane == 0) ol.brick_cnt[u] = cnt;
     hfd::wave_sync();
-    uint16_t* bh = bhist + (size_t)brick * bhist_stride(bklen);
-    for (int i = lane; i < bhist_stride(bklen); i += 64) {
-      uint32_t c = 0;
+    // unit histogram -> u16 record (16-B stores, 8 bins per lane) and the workgroup histogram
+    uint16_t* bh = bhist + (size_t)u * hs;
+    for (int i0 = lane * 8; i0 < hs; i0 += 512) {
+      uint32_t c[8];
 #pragma unroll
-      for (int j = 0; j < kHistCopies; j++) c += s_hist[i * kHistCopies + j], s_hist[i * kHistCopies + j] = 0;
-      bh[i] = (uint16_t)c;
-      if (c) atomicAdd(&s_wg[i], c);
+      for (int k = 0; k < 8; k++) {
+        c[k] = 0;
+#pragma unroll
+        for (int j = 0; j < kHistCopies; j++) c[k] += s_hist[(i0 + k) * kHistCopies + j];
+      }
+#pragma unroll
+      for (int k = 0; k < 8 * kHistCopies; k++) s_hist[i0 * kHistCopies + k] = 0;
+      *reinterpret_cast<uint4*>(bh + i0) =
+          make_uint4(c[0] | c[1] << 16, c[2] | c[3] << 16, c[4] | c[5] << 16, c[6] | c[7] << 16);
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        if (c[k]) atomicAdd(&s_wg[i0 + k], c[k]);
     }
     hfd::wave_sync();
   }
@@ -246,13 +261,16 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
 // =========================================================================================
 // plan: per-brick region sizes and outlier offsets, archive totals and headers
 // =========================================================================================
-// One launch after the codebook upload plans the whole archive:
-//  * per brick: region upper bound ub = (sum_s hist_b[s] len[s] + 31 rows) / 32 cells and its
-//    outlier count; block-local exclusive prefixes of both (kPlanBricks bricks per block);
+// One launch after the codebook upload plans the whole archive (per unit of kUnitBricks bricks;
+// "brick" below indexes units):
+//  * per unit: region upper bound ub = (sum_s hist_u[s] len[s] + 31 rows) / 32 cells and its
+//    outlier count; block-local exclusive prefixes of both (kPlanBricks units per block);
 //  * block totals by agent-scope atomics; the block that finishes last scans them (every brick's
 //    base = local prefix + block prefix), fills the size fields and writes both headers.
 // Replaces the reference's host-side scans (hf_kernels.cuhip.inl:449-473, compressor.inl:398-418).
-constexpr int kPlanBricks = 64;  // 16 bricks per wave
+constexpr int kPlanBricks = 64;  // units per plan block: 4 per wave, all loads issued together
+constexpr int kPlanThreads = 1024;
+constexpr int kPlanWaves = kPlanThreads / 64;
 
 __device__ __forceinline__ uint32_t brick_rows3(uint32_t brick, uint32_t nbx, uint32_t nby, uint32_t ly, uint32_t lz)
 {
@@ -260,32 +278,41 @@ __device__ __forceinline__ uint32_t brick_rows3(uint32_t brick, uint32_t nbx, ui
   return min(8u, ly - by * 8) * min(8u, lz - bz * 8);
 }
 
-__global__ void __launch_bounds__(256) k_brick_plan(BrickPlanArgs a, HeaderTpl tpl)
+__global__ void __launch_bounds__(kPlanThreads) k_brick_plan(BrickPlanArgs a, HeaderTpl tpl)
 {
   __shared__ uint32_t s_len[kMaxBklen];
   __shared__ uint32_t s_ub[kPlanBricks], s_oc[kPlanBricks];
-  __shared__ unsigned long long s_bits[4];
+  __shared__ unsigned long long s_bits[kPlanWaves];
   __shared__ uint32_t s_last;
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  for (int i = tid; i < a.bhs; i += 256) s_len[i] = i < a.bklen ? a.book[i] >> 27 : 0u;
+  for (int i = tid; i < a.bhs; i += kPlanThreads) s_len[i] = i < a.bklen ? a.book[i] >> 27 : 0u;
   __syncthreads();
   const uint32_t nblk = gridDim.x, b0 = blockIdx.x * kPlanBricks;
   unsigned long long wbits = 0;
-  for (int j = 0; j < kPlanBricks / 4; j++) {
-    const uint32_t slot = wid * (kPlanBricks / 4) + j, brick = b0 + slot;
+#pragma unroll
+  for (int j = 0; j < kPlanBricks / kPlanWaves; j++) {
+    const uint32_t slot = wid * (kPlanBricks / kPlanWaves) + j, brick = b0 + slot;
     uint32_t ub = 0, oc = 0;
-    if (brick < a.nbricks) {
+    if (brick < a.nunits) {
       const uint16_t* h = a.bhist + (size_t)brick * a.bhs;
       uint32_t bits = 0;
-      for (int i = lane * 8; i < a.bhs; i += 512) {
-        const uint4 v = *reinterpret_cast<const uint4*>(h + i);  // 8 bins
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      // bhs <= 1024: two 16-B loads (8 bins each) per lane
+      const int i0 = lane * 8, i1 = lane * 8 + 512;
+      const uint4 z4 = make_uint4(0, 0, 0, 0);
+      const uint4 v0 = i0 < a.bhs ? *reinterpret_cast<const uint4*>(h + i0) : z4;
+      const uint4 v1 = i1 < a.bhs ? *reinterpret_cast<const uint4*>(h + i1) : z4;
+      const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
-        for (int k = 0; k < 4; k++) bits += (w[k] & 0xFFFFu) * s_len[i + 2 * k] + (w[k] >> 16) * s_len[i + 2 * k + 1];
+      for (int k = 0; k < 8; k++) {
+        const int i = (k < 4 ? i0 : i1) + 2 * (k & 3);
+        if (i < a.bhs) bits += (w[k] & 0xFFFFu) * s_len[i] + (w[k] >> 16) * s_len[i + 1];
       }
       bits = hfd::wave_sum(bits);
       wbits += bits;
-      ub = (bits + 31u * brick_rows3(brick, a.nbx, a.nby, a.ly, a.lz)) >> 5;
+      uint32_t rows = 0;  // chunks of the unit: each may end with a partial cell
+      for (uint32_t b = brick * kUnitBricks; b < min((brick + 1) * kUnitBricks, a.nbricks); b++)
+        rows += brick_rows3(b, a.nbx, a.nby, a.ly, a.lz);
+      ub = (bits + 31u * rows) >> 5;
       oc = min(a.brick_cnt[brick], a.cap_per_brick);
     }
     if (lane == 0) s_ub[slot] = ub, s_oc[slot] = oc;
@@ -296,11 +323,13 @@ __global__ void __launch_bounds__(256) k_brick_plan(BrickPlanArgs a, HeaderTpl t
     const uint32_t ub = s_ub[lane], oc = s_oc[lane];
     const uint32_t iu = hfd::wave_incl_scan(ub), io = hfd::wave_incl_scan(oc);
     const uint32_t brick = b0 + lane;
-    if (brick < a.nbricks) a.ub[brick] = ub, a.cell_local[brick] = iu - ub, a.ol_local[brick] = io - oc;
+    if (brick < a.nunits) a.ub[brick] = ub, a.cell_local[brick] = iu - ub, a.ol_local[brick] = io - oc;
     if (lane == 63) {
       atomicExch(a.cell_pre + blockIdx.x, iu);
       atomicExch(a.ol_pre + blockIdx.x, io);
-      atomicAdd(&a.info->total_nbit, s_bits[0] + s_bits[1] + s_bits[2] + s_bits[3]);
+      unsigned long long tb = 0;
+      for (int w = 0; w < kPlanWaves; w++) tb += s_bits[w];
+      atomicAdd(&a.info->total_nbit, tb);
       const uint32_t ticket =
           __hip_atomic_fetch_add(&a.info->pad[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
       s_last = ticket == nblk - 1;
@@ -309,11 +338,11 @@ __global__ void __launch_bounds__(256) k_brick_plan(BrickPlanArgs a, HeaderTpl t
   __syncthreads();
   if (!s_last) return;
   // last block: exclusive scans of the block totals (read back by atomics: other XCDs' L2s)
-  __shared__ uint32_t s_wsum[2][4];
+  __shared__ uint32_t s_wsum[2][kPlanWaves];
   __shared__ uint32_t s_carry[2];
   if (tid < 2) s_carry[tid] = 0;
   __syncthreads();
-  for (uint32_t c0 = 0; c0 < nblk; c0 += 256) {
+  for (uint32_t c0 = 0; c0 < nblk; c0 += kPlanThreads) {
     const uint32_t i = c0 + tid;
     const uint32_t vc = i < nblk ? atomicAdd(a.cell_pre + i, 0u) : 0u;
     const uint32_t vo = i < nblk ? atomicAdd(a.ol_pre + i, 0u) : 0u;
@@ -324,7 +353,7 @@ __global__ void __launch_bounds__(256) k_brick_plan(BrickPlanArgs a, HeaderTpl t
     for (int w = 0; w < wid; w++) oc += s_wsum[0][w], oo += s_wsum[1][w];
     if (i < nblk) a.cell_pre[i] = oc + ic - vc, a.ol_pre[i] = oo + io - vo;
     __syncthreads();
-    if (tid == 255) s_carry[0] = oc + ic, s_carry[1] = oo + io;
+    if (tid == kPlanThreads - 1) s_carry[0] = oc + ic, s_carry[1] = oo + io;
     __syncthreads();
   }
   if (tid == 0) {
@@ -380,66 +409,74 @@ k_brick3_pack(const uint16_t* __restrict__ bcodes, uint32_t ly, uint32_t lz, con
       ol_dst[slot_total + i] = make_uint2((uint32_t)c, (uint32_t)(c >> 32));
     }
   }
-  for (uint32_t it = blockIdx.x * kBrickWaves + wid; it < nbricks; it += nw) {
-    const uint32_t brick = reverse ? nbricks - 1 - it : it;
-    const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
-    const uint32_t y0 = by * 8, z0 = bz * 8;
-    const uint32_t nyv = min(8u, ly - y0), nzv = min(8u, lz - z0);
-    const uint32_t pb = brick / kPlanBricks;
-    const uint32_t base = pl.cell_local[brick] + pl.cell_pre[pb], lim = pl.ub[brick];
-    {  // this brick's outlier slot -> the archive's outlier segment (brick order)
-      const uint32_t cnt = min(pl.brick_cnt[brick], pl.cap_per_brick);
-      const uint64_t* slot = pl.slots + (size_t)brick * pl.cap_per_brick;
-      uint2* d = ol_dst + pl.ol_local[brick] + pl.ol_pre[pb];
+  const uint32_t nunits = pl.nunits;
+  for (uint32_t it = blockIdx.x * kBrickWaves + wid; it < nunits; it += nw) {
+    const uint32_t unit = reverse ? nunits - 1 - it : it;
+    const uint32_t pb = unit / kPlanBricks;
+    const uint32_t base = pl.cell_local[unit] + pl.cell_pre[pb], lim = pl.ub[unit];
+    {  // this unit's outlier slot -> the archive's outlier segment (unit = brick order)
+      const uint32_t cnt = min(pl.brick_cnt[unit], pl.cap_per_brick);
+      const uint64_t* slot = pl.slots + (size_t)unit * pl.cap_per_brick;
+      uint2* d = ol_dst + pl.ol_local[unit] + pl.ol_pre[pb];
       for (uint32_t i = lane; i < cnt; i += 64) {
         const uint64_t c = slot[i];
         d[i] = make_uint2((uint32_t)c, (uint32_t)(c >> 32));
       }
     }
     uint32_t* dst = bitstream + base;
-    const uint2* src = reinterpret_cast<const uint2*>(bcodes + (size_t)brick * 64 * (64 * V)) + lane;
-    uint32_t off = 0, my_nbit = 0, my_entry = 0;
-    uint2 cur[8], nxt[8];
+    uint32_t off = 0;
+    const uint32_t bend = min((unit + 1) * kUnitBricks, nbricks);
+    for (uint32_t brick = unit * kUnitBricks; brick < bend; brick++) {
+      const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
+      const uint32_t y0 = by * 8, z0 = bz * 8;
+      const uint32_t nyv = min(8u, ly - y0), nzv = min(8u, lz - z0);
+      const uint2* src = reinterpret_cast<const uint2*>(bcodes + (size_t)brick * 64 * (64 * V)) + lane;
+      uint32_t my_nbit = 0, my_entry = 0;
+      uint2 cur[8], nxt[8];
 #pragma unroll
-    for (int z = 0; z < 8; z++) nxt[z] = (uint32_t)z < nzv ? src[z * 64] : make_uint2(0, 0);
-    for (uint32_t y = 0; y < nyv; y++) {
+      for (int z = 0; z < 8; z++) nxt[z] = (uint32_t)z < nzv ? src[z * 64] : make_uint2(0, 0);
+      for (uint32_t y = 0; y < nyv; y++) {
 #pragma unroll
-      for (int z = 0; z < 8; z++) cur[z] = nxt[z];
-      if (y + 1 < nyv)
+        for (int z = 0; z < 8; z++) cur[z] = nxt[z];
+        if (y + 1 < nyv)
 #pragma unroll
-        for (int z = 0; z < 8; z++) nxt[z] = (uint32_t)z < nzv ? src[((y + 1) * 8 + z) * 64] : make_uint2(0, 0);
+          for (int z = 0; z < 8; z++) nxt[z] = (uint32_t)z < nzv ? src[((y + 1) * 8 + z) * 64] : make_uint2(0, 0);
 #pragma unroll
-      for (int z = 0; z < 8; z++) {
-        if ((uint32_t)z >= nzv) break;
-        const uint32_t qs[4] = {cur[z].x & 0xFFFFu, cur[z].x >> 16, cur[z].y & 0xFFFFu, cur[z].y >> 16};
-        uint32_t w[V], bits = 0;
+        for (int z = 0; z < 8; z++) {
+          if ((uint32_t)z >= nzv) break;
+          const uint32_t qs[4] = {cur[z].x & 0xFFFFu, cur[z].x >> 16, cur[z].y & 0xFFFFu, cur[z].y >> 16};
+          uint32_t w[V], bits = 0;
 #pragma unroll
-        for (int k = 0; k < V; k++) {
-          w[k] = s_book[qs[k]];
-          bits += w[k] >> 27;
+          for (int k = 0; k < V; k++) {
+            w[k] = s_book[qs[k]];
+            bits += w[k] >> 27;
+          }
+          const uint32_t inc = hfd::wave_incl_scan(bits);
+          const uint32_t tot = readlane(inc, 63);
+          if (__builtin_expect(__builtin_amdgcn_ballot_w64(bits > 64u) == 0, 1))
+            hfd::pack4_or(cells, inc - bits, w, bits);
+          else
+            hfd::pack_words<V>(cells, inc - bits, w, V);
+          hfd::wave_sync();
+          const uint32_t nc = (tot + 31) >> 5;
+          for (uint32_t i = lane; i < nc; i += 64) {
+            if (off + i < lim) dst[off + i] = cells[i];
+            cells[i] = 0;
+          }
+          if ((uint32_t)lane == y * 8 + z) my_nbit = tot, my_entry = base + off;
+          off += nc;
+          hfd::wave_sync();
         }
-        const uint32_t inc = hfd::wave_incl_scan(bits);
-        const uint32_t tot = readlane(inc, 63);
-        hfd::pack_words<V>(cells, inc - bits, w, V);
-        hfd::wave_sync();
-        const uint32_t nc = (tot + 31) >> 5;
-        for (uint32_t i = lane; i < nc; i += 64) {
-          if (off + i < lim) dst[off + i] = cells[i];
-          cells[i] = 0;
-        }
-        if ((uint32_t)lane == y * 8 + z) my_nbit = tot, my_entry = base + off;
-        off += nc;
-        hfd::wave_sync();
+      }
+      const uint32_t ry = lane >> 3, rz = lane & 7;
+      if (ry < nyv && rz < nzv) {
+        const size_t c = ((size_t)(z0 + rz) * ly + (y0 + ry)) * nbx + bx;
+        par_nbit[c] = my_nbit;
+        par_entry[c] = my_entry;
       }
     }
     if (off > lim && lane == 0) atomicOr(overflow, 1u);  // cannot happen (region is an upper bound)
     for (uint32_t i = off + lane; i < lim; i += 64) dst[i] = 0u;
-    const uint32_t ry = lane >> 3, rz = lane & 7;
-    if (ry < nyv && rz < nzv) {
-      const size_t c = ((size_t)(z0 + rz) * ly + (y0 + ry)) * nbx + bx;
-      par_nbit[c] = my_nbit;
-      par_entry[c] = my_entry;
-    }
   }
 }
 
@@ -852,11 +889,12 @@ int launch_brick_plan(const BrickLaunch& L, const BrickPlanArgs& a, const void* 
   HeaderTpl t;
   __builtin_memcpy(t.psz, psz_tpl, 176);
   __builtin_memcpy(t.phf, phf_tpl, 64);
-  k_brick_plan<<<a.nblk, 256, 0, st>>>(a, t);
+  k_brick_plan<<<a.nblk, kPlanThreads, 0, st>>>(a, t);
   return (int)hipGetLastError();
 }
 
-uint32_t brick_plan_blocks(uint32_t nbricks) { return (nbricks + kPlanBricks - 1) / kPlanBricks; }
+uint32_t brick_units(uint32_t nbricks) { return (nbricks + kUnitBricks - 1) / kUnitBricks; }
+uint32_t brick_plan_blocks(uint32_t nbricks) { return (brick_units(nbricks) + kPlanBricks - 1) / kPlanBricks; }
 int brick_hist_stride(int bklen) { return bhist_stride(bklen); }
 
 int launch_brick_pack(const BrickLaunch& L, const uint16_t* bcodes, const uint32_t* book, int bklen,

@@ -69,6 +69,28 @@ __device__ __forceinline__ void pack_words(uint32_t* cells, uint32_t pos, const 
   if (fill) atomicOr(&cells[q], (uint32_t)(acc >> 32));
 }
 
+// Same result as pack_words<4> for a lane whose 4 codewords total L <= 64 bits: Horner-pack them
+// right-aligned into 64 bits (shift by the length, OR the code into the low word), align the
+// stream end to a word boundary and OR the (up to) three words ending at word (pos+L-1)/32 into
+// the zeroed LDS cells.  Words of the lane's range not covered by its bits receive 0.
+__device__ __forceinline__ void pack4_or(uint32_t* cells, uint32_t pos, const uint32_t (&w)[4], uint32_t L)
+{
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    acc <<= (w[k] >> 27);
+    acc |= w[k] & 0x07FFFFFFu;
+  }
+  const uint32_t e = pos + L, E = (e - 1) >> 5, t = (32u - (e & 31u)) & 31u;
+  const uint32_t lo = (uint32_t)acc, hi = (uint32_t)(acc >> 32);
+  const uint32_t w2 = lo << t;
+  const uint32_t w1 = t ? __builtin_amdgcn_alignbit(hi, lo, 32u - t) : hi;
+  const uint32_t w0 = t ? hi >> (32u - t) : 0u;
+  atomicOr(&cells[E], w2);
+  if (E >= 1) atomicOr(&cells[E - 1], w1);
+  if (E >= 2) atomicOr(&cells[E - 2], w0);
+}
+
 // ---- decode tables --------------------------------------------------------------------------
 // Entry (u32) for the codeword(s) at the top of a window: [9:0] first symbol, [25:16] second
 // symbol, [30:26] bits consumed, [31] two symbols.  0 = not in this table.  The symbols sit

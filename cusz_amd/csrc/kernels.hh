@@ -195,10 +195,10 @@ struct BrickPlanArgs {
   const uint16_t* bhist;  // per-brick histograms, stride brick_hist_stride(bklen)
   int bklen, bhs;
   const uint32_t* book;
-  uint32_t nbricks, nbx, nby, ly, lz;
-  const uint32_t* brick_cnt;  // outliers per brick (pass 1)
-  uint32_t cap_per_brick;
-  const uint64_t* slots;      // per-brick outlier slots
+  uint32_t nbricks, nunits, nbx, nby, ly, lz;  // units of brick_units(): regions, slots, histograms
+  const uint32_t* brick_cnt;  // outliers per unit (pass 1)
+  uint32_t cap_per_brick;     // outlier slot capacity per unit
+  const uint64_t* slots;      // per-unit outlier slots
   const uint64_t* spill;
   const uint32_t* spill_cnt;
   uint32_t spill_cap;
@@ -212,6 +212,7 @@ struct BrickPlanArgs {
   uint8_t* archive;
   size_t phf_offset, bitstream_rel;
 };
+uint32_t brick_units(uint32_t nbricks);
 uint32_t brick_plan_blocks(uint32_t nbricks);
 int brick_hist_stride(int bklen);
 int launch_brick_plan(const BrickLaunch& L, const BrickPlanArgs& a, const void* psz_tpl, const void* phf_tpl,

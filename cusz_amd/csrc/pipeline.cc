@@ -160,7 +160,12 @@ struct Pipeline {
   }
 
   size_t rvbk_bytes(int bklen) const { return 4 * 64 + 2 * (size_t)bklen; }
-  uint32_t brick_cap() const { return bl.g.brick_elems / 10 + 16; }
+  // outlier slot per brick unit (brick.hip kUnitBricks bricks): 10 % of its elements + 16
+  uint32_t brick_cap() const
+  {
+    const uint32_t nu = brick_units(bl.g.nbricks), per = (bl.g.nbricks + nu - 1) / nu;
+    return (uint32_t)((size_t)bl.g.brick_elems * per / 10 + 16);
+  }
   unsigned int* work_counter() { return reinterpret_cast<unsigned int*>(d_small + kSmallBytes - kWorkBytes); }
 
   // fused brick path: 3-D, eligible shape, Lorenzo, default chunking (chunk = brick row)
@@ -279,9 +284,26 @@ struct Pipeline {
     return ms;
   }
 
+  // state carried from compress_scan (pass 1) to compress_finish (codebook onwards)
+  struct Pending {
+    bool active = false, brick = false, spl = false;
+    int radius = 0;
+    size_t anchor_bytes = 0;
+  } pend;
+
   template <typename T>
   int compress(psz_header* h, const T* in, uint8_t** out, size_t* outlen)
   {
+    const int s = compress_scan<T>(h, in);
+    return s ? s : compress_finish(h, nullptr, out, outlen);
+  }
+
+  // Pass 1: [extrema] -> predict + histogram + outliers (+ codes).  The histogram stays on the
+  // device (d_hist) for compress_finish, or for a caller that reduces it across slabs first.
+  template <typename T>
+  int compress_scan(psz_header* h, const T* in)
+  {
+    pend.active = false;
     const psz_predictor pred = h->pipeline.predictor;
     if (pred != Lorenzo && pred != LorenzoZigZag && pred != Spline) return PSZ_ABORT_NO_SUCH_PREDICTOR;
     if (h->pipeline.codec1 != Huffman) return PSZ_ABORT_NO_SUCH_CODEC;
@@ -327,7 +349,16 @@ struct Pipeline {
     if (!brick) CUSZ_AMD_HIP_CHECK(hipMemsetAsync(d_status, 0, status_words * 8, stream));
     mark(1);
     last_layout = brick ? PSZ_AMD_LAYOUT_BRICK : PSZ_AMD_LAYOUT_REFERENCE;
-    if (brick) return compress_brick<T>(h, in, out, outlen, eb, radius, zz);
+    pend.brick = brick, pend.spl = spl, pend.radius = radius;
+    pend.anchor_bytes = spl ? sizeof(T) * sgeom.anchor_len : 0;
+    if (brick) {
+      OutlierSink bol{d_slots, d_brick_cnt, d_spill, spill_cnt(), brick_cap(), spill_cap, nullptr};
+      CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_scan<T>(bl, in, eb, radius, zz, bol, d_hist, d_bhist, d_codes,
+                                                          bklen, stream));
+      mark(2);
+      pend.active = true;
+      return PSZ_SUCCESS;
+    }
 
     const size_t anchor_bytes = spl ? sizeof(T) * sgeom.anchor_len : 0;
     uint64_t* slots = spl ? d_spl_slots : d_slots;
@@ -360,6 +391,27 @@ struct Pipeline {
                                                          ol, d_hist, bklen, stream));
     }
     mark(2);
+    pend.active = true;
+    return PSZ_SUCCESS;
+  }
+
+  // Codebook (from d_hist, or from `ext_hist`: a device u32[bklen] the caller reduced across
+  // slabs) -> encode -> archive.
+  int compress_finish(psz_header* h, const uint32_t* ext_hist, uint8_t** out, size_t* outlen)
+  {
+    if (!pend.active) return PSZ_ABORT_NOT_IMPLEMENTED;
+    pend.active = false;
+    const int radius = pend.radius, bklen = 2 * radius;
+    if (ext_hist) CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(d_hist, ext_hist, (size_t)bklen * 4, hipMemcpyDeviceToDevice, stream));
+    if (pend.brick) return compress_brick(h, out, outlen, radius);
+    const bool spl = pend.spl;
+    const size_t anchor_bytes = pend.anchor_bytes;
+    uint64_t* slots = spl ? d_spl_slots : d_slots;
+    uint32_t* bcnt = spl ? d_spl_cnt : d_brick_cnt;
+    uint32_t* boff = spl ? d_spl_off : d_brick_off;
+    const uint32_t nbr = spl ? sgeom.ntiles : geom.nbricks;
+    const uint32_t cap = spl ? spl_cap : cap_per_brick;
+    uint32_t* spill_start = spl ? d_spl_sps : nullptr;
 
     // codebook on the host (hf_hl.cc:21-34), one round trip
     int fs = fetch(regions({{h_hist(), d_hist, (size_t)bklen * 4}}), 2);
@@ -389,10 +441,10 @@ struct Pipeline {
     mark(4);
 
     FinalizeArgs fa{ea.par_nbit, ea.par_entry, pardeg, bcnt, nbr, cap, spill_cnt(), spill_cap, boff, info(),
-                    ol.spill_start};
+                    spill_start};
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_finalize_scan(fa, stream));
     OutlierCopyArgs oa{slots, bcnt,      boff,           nbr, cap, d_spill, spill_cnt(), spill_cap,
-                       info(), d_archive, phf_off + bits_rel, ol.spill_start};
+                       info(), d_archive, phf_off + bits_rel, spill_start};
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_outlier_copy(oa, stream));
 
     // header templates: static fields from the host, dynamic ones filled on the device
@@ -413,18 +465,12 @@ struct Pipeline {
 
   // Fused brick compress (brick.hip): pass 1 (histograms + outliers) -> host codebook ->
   // region reservation -> pass 2 (predict + pack straight into the archive) -> finalize.
-  template <typename T>
-  int compress_brick(psz_header* h, const T* in, uint8_t** out, size_t* outlen, double eb, int radius, bool zz)
+  int compress_brick(psz_header* h, uint8_t** out, size_t* outlen, int radius)
   {
     const int bklen = 2 * radius;
     const BrickGeom& g = bl.g;
     const int bsub = g.W, bpar = (int)g.nchunks;
     const uint32_t cap = brick_cap();
-    OutlierSink ol{d_slots, d_brick_cnt, d_spill, spill_cnt(), cap, spill_cap, nullptr};
-    CUSZ_AMD_HIP_CHECK(
-        (hipError_t)launch_brick_scan<T>(bl, in, eb, radius, zz, ol, d_hist, d_bhist, d_codes, bklen, stream));
-    mark(2);
-
     int fs = fetch(regions({{h_hist(), d_hist, (size_t)bklen * 4}}), 2);
     if (fs) return fs;
     const int rv = build_codebook(h_hist(), bklen, h_book(), h_revbook());
@@ -452,7 +498,7 @@ struct Pipeline {
     ph.entry[4] = (uint32_t)bits_rel;
 
     const uint32_t nblk = brick_plan_blocks(g.nbricks);
-    BrickPlanArgs pa{d_bhist, bklen, brick_hist_stride(bklen), d_book, g.nbricks, g.nbx, g.nby, bl.ly, bl.lz,
+    BrickPlanArgs pa{d_bhist, bklen, brick_hist_stride(bklen), d_book, g.nbricks, brick_units(g.nbricks), g.nbx, g.nby, bl.ly, bl.lz,
                      d_brick_cnt, cap, d_slots, d_spill, spill_cnt(), spill_cap, nblk, d_ub, d_bbase, d_brick_off,
                      d_plan, d_plan + nblk + 1, info(), d_archive, phf_off, bits_rel};
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_plan(bl, pa, h, &ph, stream));
@@ -726,9 +772,36 @@ static int compress_impl(psz_resource* m, psz_rc2 rc, T* in, psz_header* out_h, 
   m->header->rc = rc;
   m->header->user_input_eb = rc.eb;
   m->dict_size = (uint16_t)(rc.radius * 2);
+  CUSZ_AMD_HIP_CHECK(hipSetDevice(p->device));  // the creation device (B.7; several GPUs per process)
   int s = p->compress<T>(m->header, in, out, outlen);
   if (out_h) *out_h = *m->header;
   return s != PSZ_SUCCESS ? s : status;
+}
+
+template <typename T>
+static int scan_impl(psz_resource* m, psz_rc2 rc, T* in)
+{
+  if (!m || !in) return PSZ_ABORT_NOT_IMPLEMENTED;
+  Pipeline* p = cusz_amd::P(m);
+  if ((sizeof(T) == 4) != (m->header->dtype == F4)) return PSZ_ABORT_UNSUPPORTED_TYPE;
+  int status = PSZ_SUCCESS;
+  if (rc.radius > 512) rc.radius = 512, status = PSZ_WARN_RADIUS_TOO_LARGE;  // libcusz.cc:281-285
+  m->header->rc = rc;
+  m->header->user_input_eb = rc.eb;
+  m->dict_size = (uint16_t)(rc.radius * 2);
+  CUSZ_AMD_HIP_CHECK(hipSetDevice(p->device));
+  const int s = p->compress_scan<T>(m->header, in);
+  return s != PSZ_SUCCESS ? s : status;
+}
+
+// copy the slab histogram (device) to the caller's device buffer, on the manager's stream
+static int export_hist(psz_resource* m, uint32_t* d_out, int status)
+{
+  Pipeline* p = cusz_amd::P(m);
+  if (!d_out) return PSZ_ABORT_NOT_IMPLEMENTED;
+  CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(d_out, p->d_hist, sizeof(uint32_t) * 2 * m->header->rc.radius,
+                                    hipMemcpyDeviceToDevice, p->stream));
+  return status;
 }
 
 extern "C" {
@@ -746,13 +819,39 @@ int psz_compress_double(psz_resource* m, psz_rc2 rc, double* in, psz_header* out
 
 int psz_compress_analyize_float(psz_resource* m, psz_rc2 rc, float* in, u4* exported_h_hist)
 {
-  // compressor.inl:305-337: predict + histogram, export the histogram to the host
-  uint8_t* dummy;
-  size_t bytes;
-  int s = compress_impl<float>(m, rc, in, nullptr, &dummy, &bytes);
+  // compressor.inl:305-337: predict + histogram only, the histogram exported to the host
+  if (!exported_h_hist) return PSZ_ABORT_NOT_IMPLEMENTED;
+  const int s = scan_impl<float>(m, rc, in);
   if (s != PSZ_SUCCESS && s != PSZ_WARN_RADIUS_TOO_LARGE) return s;
   Pipeline* p = cusz_amd::P(m);
-  std::memcpy(exported_h_hist, p->h_hist(), sizeof(u4) * 2 * m->header->rc.radius);
+  const size_t bytes = sizeof(u4) * 2 * m->header->rc.radius;
+  const int fs = p->fetch(Pipeline::regions({{p->h_hist(), p->d_hist, bytes}}), 2);
+  p->pend.active = false;
+  if (fs) return fs;
+  std::memcpy(exported_h_hist, p->h_hist(), bytes);
+  return s;
+}
+
+int psz_amd_compress_scan_float(psz_resource* m, psz_rc2 rc, float* in, uint32_t* d_hist_out)
+{
+  const int s = scan_impl<float>(m, rc, in);
+  return (s == PSZ_SUCCESS || s == PSZ_WARN_RADIUS_TOO_LARGE) ? export_hist(m, d_hist_out, s) : s;
+}
+
+int psz_amd_compress_scan_double(psz_resource* m, psz_rc2 rc, double* in, uint32_t* d_hist_out)
+{
+  const int s = scan_impl<double>(m, rc, in);
+  return (s == PSZ_SUCCESS || s == PSZ_WARN_RADIUS_TOO_LARGE) ? export_hist(m, d_hist_out, s) : s;
+}
+
+int psz_amd_compress_finish(psz_resource* m, const uint32_t* d_hist, psz_header* out_h, uint8_t** out,
+                            size_t* outlen)
+{
+  Pipeline* p = cusz_amd::P(m);
+  if (!p || !out || !outlen) return PSZ_ABORT_NOT_IMPLEMENTED;
+  CUSZ_AMD_HIP_CHECK(hipSetDevice(p->device));
+  const int s = p->compress_finish(m->header, d_hist, out, outlen);
+  if (out_h) *out_h = *m->header;
   return s;
 }
 
@@ -765,6 +864,7 @@ static int decompress_impl(psz_resource* m, uint8_t* in, size_t in_len, T* out)
   (void)in_len;
   Pipeline* p = cusz_amd::P(m);
   if ((sizeof(T) == 4) != (m->header->dtype == F4)) return PSZ_ABORT_UNSUPPORTED_TYPE;
+  CUSZ_AMD_HIP_CHECK(hipSetDevice(p->device));
   int s = p->decompress<T>(m->header, in, out);
   if (s == PSZ_SUCCESS && p->timing) p->collect_decompress_times();
   return s;

@@ -1,13 +1,21 @@
 """Multi-GPU sharding of the cuSZ hot path (one process per GPU, torch.distributed/RCCL).
 
-The reference has no multi-GPU code (SURVEY.md §0.6).  The path shards naturally because
+The reference has no multi-GPU code (SURVEY.md §0.6, §8e).  The path shards naturally because
 prediction is tile-local (lrz_c.cuhip.inl: no halo): a slab whose boundaries fall on tile
 boundaries -- 8 planes in z (3-D), 32 rows in y (2-D), 1024 elements (1-D) -- yields exactly
-the quant codes and outliers the single-GPU run produces for those elements.  Each rank
-compresses its slab (or its own independent field) with its own manager: no data-path
-collective.  The only exchange is gathering the per-rank archives to a root for output:
-sizes by all_gather (8 B per rank), then the archive bytes (padded to the max size) by
-all_gather_into_tensor -- over RCCL/xGMI for device tensors, gloo for host tensors.
+the quant codes and outliers the single-GPU run produces for those elements.
+
+Exchange steps (the only collectives; everything else is rank-local):
+  1. optional global codebook: every rank runs pass 1 on its slab
+     (psz_amd_compress_scan_*), the u32[bklen] histograms of all fields are summed by ONE
+     all-reduce (``allreduce_histograms``: [fields, bklen] int64, 8 KB per field), and every
+     rank finishes its slabs with the same codebook (psz_amd_compress_finish);
+  2. gather of the per-rank archives to ONE root (``gather_to_root``): 8-B sizes by
+     all_gather, then exact-size point-to-point sends to the root (batch_isend_irecv ->
+     grouped ncclSend/ncclRecv over xGMI on GPUs, gloo on CPU) -- no max-size padding and no
+     bytes to non-root ranks;
+  3. the root merges the slabs of one field into the single archive a one-process run would
+     have written (``merge``: psz_amd_merge_archives, host code).
 """
 from __future__ import annotations
 
@@ -56,6 +64,70 @@ def plan_slabs(dims, world: int):
         out.append(Slab(r, lo * stride, tuple(d), start_tile))
         start_tile += nt
     return out
+
+
+def gather_to_root(buf, dist, root: int = 0):
+    """Gather one variable-length uint8 tensor per rank to `root` only: sizes by all_gather
+    (one int64 per rank), bytes by exact-size point-to-point transfers.  Returns the list of
+    per-rank tensors (rank order) on `root`, None elsewhere.  Device tensors go over RCCL
+    (grouped ncclSend/ncclRecv), host tensors over gloo."""
+    import torch
+
+    world, rank = dist.get_world_size(), dist.get_rank()
+    n = torch.tensor([buf.numel()], dtype=torch.int64, device=buf.device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    sizes = [int(s.item()) for s in sizes]
+    if rank != root:
+        if sizes[rank]:
+            for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, buf.contiguous(), root)]):
+                w.wait()
+        return None
+    out = [buf if r == root else torch.empty(sizes[r], dtype=torch.uint8, device=buf.device)
+           for r in range(world)]
+    ops = [dist.P2POp(dist.irecv, out[r], r) for r in range(world) if r != root and sizes[r]]
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    return out
+
+
+def allreduce_histograms(hists, dist):
+    """Sum the u32 histograms of every rank's slabs in one all-reduce.  `hists`: int64 tensor
+    [fields, bklen] (device for RCCL, host for gloo); summed in place and returned."""
+    dist.all_reduce(hists, op=dist.ReduceOp.SUM)
+    return hists
+
+
+def compress_fields_sharded(resources, d_ptrs, eb, dist, mode=0, radius=512, device=None):
+    """Sharded compress of several fields whose slabs this rank holds, with one codebook per
+    field shared by all ranks: pass 1 per slab, ONE all-reduce of the [fields, bklen]
+    histograms, then finish every slab.  Returns [(archive_ptr, nbytes)] (device archives,
+    valid until the manager's next compress)."""
+    import torch
+
+    bklen = 2 * radius
+    f = len(resources)
+    h32 = torch.zeros((f, bklen), dtype=torch.int32, device=device)
+    for i, (r, p) in enumerate(zip(resources, d_ptrs)):
+        r.compress_scan(p, eb, h32[i].data_ptr(), mode, radius)
+    torch.cuda.synchronize(device)  # the scans run on the managers' streams
+    h64 = h32.to(torch.int64)
+    allreduce_histograms(h64, dist)
+    g32 = h64.to(torch.int32).contiguous()  # u32 bit pattern (sums < 2^32)
+    torch.cuda.synchronize(device)  # g32 is read on the managers' streams
+    out = []
+    for i, r in enumerate(resources):
+        ptr, nb, _ = r.compress_finish(g32[i].data_ptr())
+        out.append((ptr, nb))
+    return out
+
+
+def merge(parts, full_dims, offsets=None) -> bytes:
+    """Merge per-slab archives (host bytes, field order) into the whole field's archive."""
+    from . import merge_archives
+
+    return merge_archives(parts, full_dims, offsets)
 
 
 def gather_bytes(buf, dist, root: int = 0):

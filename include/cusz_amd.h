@@ -79,6 +79,31 @@ int psz_amd_set_decoder(psz_resource* m, int kind);
 #define PSZ_AMD_LAYOUT_REFERENCE 1
 int psz_amd_set_layout(psz_resource* m, int layout);
 
+/* ---- sharded compress (multi-GPU; the reference has no multi-GPU path) ----
+ * A field split into tile-aligned slabs (z: multiples of 8 planes) is compressed one slab per
+ * GPU with ONE codebook:
+ *   1. psz_amd_compress_scan_*: pass 1 only (predict, histogram, outliers); the slab's
+ *      histogram u32[2 * radius] is copied to OUT_d_hist (device, on the manager's stream).
+ *   2. the caller sums the histograms of all slabs (e.g. an RCCL all-reduce).
+ *   3. psz_amd_compress_finish: codebook from IN_d_hist (device u32[2 * radius]; NULL: the
+ *      slab's own histogram), encode, archive -- outputs as psz_compress_float.
+ * psz_compress_analyize_float (cusz_rev1.h) is step 1 with the histogram exported to the host
+ * (compressor.inl:305-337). */
+int psz_amd_compress_scan_float(psz_resource* m, psz_rc2 rc, float* IN_d_data, uint32_t* OUT_d_hist);
+int psz_amd_compress_scan_double(psz_resource* m, psz_rc2 rc, double* IN_d_data, uint32_t* OUT_d_hist);
+int psz_amd_compress_finish(psz_resource* m, const uint32_t* IN_d_hist, psz_header* OUT_header,
+                            uint8_t** OUT_d_compressed, size_t* OUT_compressed_bytes);
+
+/* Merge per-slab archives (HOST memory, in field order) compressed with one shared codebook
+ * into the archive of the whole field: the archive one process would have written for it
+ * (chunks concatenated, par_entry rebased by the cells before each slab, outlier indices by
+ * the slab's element offset).  elem_offsets (may be NULL) are checked against the running
+ * sum.  *out_bytes receives the merged size even when out_cap is too small (then nonzero is
+ * returned and nothing is written). */
+int psz_amd_merge_archives(const uint8_t* const* parts, const size_t* part_bytes, int nparts,
+                           const size_t* elem_offsets, psz_len full_len, uint8_t* out, size_t out_cap,
+                           size_t* out_bytes);
+
 const char* psz_amd_version(void);
 
 #ifdef __cplusplus

@@ -1,0 +1,98 @@
+"""Sharded compress on the GPU, one process standing in for the ranks: every
+slab is compressed by its own manager with pass 1 (psz_amd_compress_scan_*), the slab
+histograms are summed (the all-reduce's arithmetic), every slab is finished with the shared
+codebook (psz_amd_compress_finish), and psz_amd_merge_archives joins them.  The merged archive
+must be byte-identical to the archive of one compress over the whole field, in both layouts,
+and decompress to the same field."""
+import numpy as np
+import pytest
+import torch
+
+import cusz_amd as cz
+from cusz_amd import datagen
+from cusz_amd.shard import merge, plan_slabs
+from gpu_util import d2h, sync, to_device
+
+pytestmark = pytest.mark.gpu
+
+
+def _whole(data, dims, eb, dtype, layout, sublen):
+    r = cz.Resource(cz.F4 if dtype == np.float32 else cz.F8, dims)
+    r.set_layout(layout)
+    if sublen:
+        r.set_sublen(sublen)
+    ptr, nb, _ = r.compress(to_device(data).data_ptr(), eb)
+    return d2h(ptr, nb).tobytes(), r
+
+
+def _sharded(data, dims, world, eb, dtype, layout, sublen):
+    slabs = [s for s in plan_slabs(dims, world) if s.count]
+    res, dins = [], []
+    hists = torch.zeros((len(slabs), 1024), dtype=torch.int32, device="cuda")
+    for i, s in enumerate(slabs):
+        r = cz.Resource(cz.F4 if dtype == np.float32 else cz.F8, s.dims)
+        r.set_layout(layout)
+        if sublen:
+            r.set_sublen(sublen)
+        d = to_device(data[s.offset:s.offset + s.count])
+        r.compress_scan(d.data_ptr(), eb, hists[i].data_ptr())
+        res.append(r), dins.append(d)
+    sync()
+    g = hists.to(torch.int64).sum(0).to(torch.int32).contiguous()
+    parts = []
+    for r in res:
+        ptr, nb, _ = r.compress_finish(g.data_ptr())
+        parts.append(d2h(ptr, nb).tobytes())
+    return merge(parts, dims, [s.offset for s in slabs])
+
+
+@pytest.mark.parametrize("dims,world,dtype,layout,sublen", [
+    ((256, 32, 40), 2, np.float32, cz.LAYOUT_BRICK, 0),
+    ((256, 32, 40), 3, np.float32, cz.LAYOUT_BRICK, 0),
+    ((512, 24, 64), 4, np.float32, cz.LAYOUT_BRICK, 0),
+    ((256, 16, 24), 3, np.float64, cz.LAYOUT_BRICK, 0),
+    ((256, 32, 40), 3, np.float32, cz.LAYOUT_REFERENCE, 256),
+    ((96, 40, 48), 2, np.float32, cz.LAYOUT_REFERENCE, 768),
+])
+def test_sharded_merge_equals_whole_field(dims, world, dtype, layout, sublen):
+    data = datagen.smooth3d_np(dims, 31, dtype=dtype)
+    eb = 1e-4
+    single, r = _whole(data, dims, eb, dtype, layout, sublen)
+    merged = _sharded(data, dims, world, eb, dtype, layout, sublen)
+    assert len(merged) == len(single)
+    assert merged == single
+    # the merged archive decompresses through the ordinary API
+    d_arch = torch.frombuffer(bytearray(merged), dtype=torch.uint8).cuda()
+    out = torch.full((data.size,), float("nan"), dtype=torch.float32 if dtype == np.float32 else torch.float64,
+                     device="cuda")
+    r.decompress(d_arch.data_ptr(), len(merged), out.data_ptr())
+    sync()
+    err = np.abs(out.cpu().numpy().astype(np.float64) - data.astype(np.float64)).max()
+    assert err <= 1.001 * eb
+
+
+def test_scan_then_finish_equals_compress():
+    dims = (256, 24, 16)
+    data = datagen.smooth3d_np(dims, 7)
+    single, _ = _whole(data, dims, 1e-4, np.float32, cz.LAYOUT_BRICK, 0)
+    r = cz.Resource(cz.F4, dims)
+    d = to_device(data)
+    h = torch.zeros(1024, dtype=torch.int32, device="cuda")
+    r.compress_scan(d.data_ptr(), 1e-4, h.data_ptr())
+    ptr, nb, _ = r.compress_finish(0)  # the slab's own histogram
+    assert d2h(ptr, nb).tobytes() == single
+    sync()
+    assert int(h.sum().item()) == data.size  # the exported slab histogram
+
+
+def test_analyze_exports_histogram(oracle):
+    dims = (96, 64, 24)
+    data = datagen.smooth3d_np(dims, 2)
+    r = cz.Resource(cz.F4, dims)
+    d = to_device(data)
+    hist = np.zeros(1024, np.uint32)
+    st = cz.lib().psz_compress_analyize_float(r._h, cz.psz_rc2(cz.Abs, 1e-4, 512), cz.C.c_void_p(d.data_ptr()),
+                                              hist.ctypes.data_as(cz.C.c_void_p))
+    assert st == cz.PSZ_SUCCESS
+    codes, _, _ = oracle.lorenzo_c(data, dims, 1e-4)
+    np.testing.assert_array_equal(hist, oracle.histogram(codes))

@@ -64,3 +64,127 @@ def test_gather_bytes_gloo_world2():
         p.join(timeout=60)
     assert [len(g) for g in got] == [100, 137]
     assert got[1] == [v & 0xFF for v in range(137)]
+
+
+# ---------------------------------------------------------------------------------------------
+# Sharded compress with one global codebook: per-rank slab archives merged at
+# the root must equal, byte for byte, the archive one process writes for the whole field.
+# Per-slab archives are built by the CPU oracle (no GPU here); the exchange (histogram
+# all-reduce, gather to root) and the merge are the product code (cusz_amd.shard,
+# psz_amd_merge_archives).
+def oracle_archive(oracle, codes, ol_val, ol_idx, dims, eb, book, rv, sublen, bklen=1024):
+    """Reference-layout archive (psz_header | phf segment | outlier cells) from oracle codes and
+    a given codebook (hf_buf.cc:191-211, compressor.inl:398-418)."""
+    import cusz_amd as cz
+
+    nbit, entry, bs, tot = oracle.hf_encode(codes, book, sublen)
+    pardeg = nbit.size
+    sizes = [oracle.PHF_FORCED_ALIGN, rv.size, 4 * pardeg, 4 * pardeg, 4 * bs.size]
+    ent = [0]
+    for s in sizes:
+        ent.append(ent[-1] + s)
+    phf = oracle.phf_header_bytes(bklen, sublen, pardeg, codes.size, tot, bs.size, ent)
+    phf += b"\0" * (oracle.PHF_FORCED_ALIGN - len(phf)) + rv.tobytes() + nbit.tobytes() + \
+        entry.tobytes() + bs.tobytes()
+    cells = np.empty((ol_idx.size, 2), np.uint32)
+    cells[:, 0] = np.asarray(ol_val, np.float32).view(np.uint32)
+    cells[:, 1] = ol_idx
+    h = cz.psz_header()
+    h.dtype, h.pipeline.predictor, h.pipeline.codec1 = cz.F4, cz.Lorenzo, cz.Huffman
+    h.rc.mode, h.rc.eb, h.rc.radius = cz.Abs, eb, bklen // 2
+    h.vle_sublen, h.vle_pardeg = sublen, pardeg
+    h.len.x, h.len.y, h.len.z = dims
+    h.splen = ol_idx.size
+    h.user_input_eb = eb
+    e = [0, 176, 176, 176 + len(phf), 176 + len(phf) + 8 * ol_idx.size, 176 + len(phf) + 8 * ol_idx.size]
+    for i, v in enumerate(e):
+        h.entry[i] = v
+    return bytes(h) + phf + cells.tobytes()
+
+
+def _sharded_worker(rank, world, port, dims, q):
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import pyoracle as oracle
+
+    from cusz_amd import shard
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eb = 1e-4
+    data = datagen.smooth3d_np(dims, 21)
+    s = plan_slabs(dims, world)[rank]
+    codes, ov, oi = oracle.lorenzo_c(data[s.offset:s.offset + s.count], s.dims, eb)
+    hist = torch.from_numpy(oracle.histogram(codes).astype(np.int64)).reshape(1, -1)
+    shard.allreduce_histograms(hist, dist)                      # exchange 1: one all-reduce
+    book, rv = oracle.codebook(hist[0].numpy().astype(np.uint32))
+    part = oracle_archive(oracle, codes, ov, oi, s.dims, eb, book, rv, sublen=256)
+    got = shard.gather_to_root(torch.frombuffer(bytearray(part), dtype=torch.uint8), dist, 0)  # exchange 2
+    if rank == 0:
+        merged = shard.merge([g.numpy().tobytes() for g in got], dims,
+                             [p.offset for p in plan_slabs(dims, world)])
+        q.put(merged)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_merged_archive_equals_single_process(oracle, world):
+    dims = (64, 40, 48)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29600 + world * 17 + os.getpid() % 500
+    ps = [ctx.Process(target=_sharded_worker, args=(r, world, port, dims, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    merged = q.get(timeout=180)
+    for p in ps:
+        p.join(timeout=60)
+    data = datagen.smooth3d_np(dims, 21)
+    codes, ov, oi = oracle.lorenzo_c(data, dims, 1e-4)
+    book, rv = oracle.codebook(oracle.histogram(codes))
+    single = oracle_archive(oracle, codes, ov, oi, dims, 1e-4, book, rv, sublen=256)
+    assert len(merged) == len(single)
+    assert merged == single
+
+
+def _gather_worker(rank, world, port, q):
+    from cusz_amd import shard
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    buf = (torch.arange(50 + 91 * rank, dtype=torch.int32) * (rank + 1)).to(torch.uint8)
+    got = shard.gather_to_root(buf, dist, root=1)
+    q.put((rank, None if got is None else [g.tolist() for g in got]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_to_root_exact_sizes_gloo_world3():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29700 + os.getpid() % 500
+    ps = [ctx.Process(target=_gather_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(3))
+    for p in ps:
+        p.join(timeout=60)
+    assert res[0] is None and res[2] is None  # only the root receives
+    assert [len(g) for g in res[1]] == [50, 141, 232]
+    assert res[1][2] == [(v * 3) & 0xFF for v in range(232)]
+
+
+def test_merge_rejects_mismatched_codebooks(oracle):
+    import cusz_amd as cz
+
+    dims = (64, 40, 16)
+    data = datagen.smooth3d_np(dims, 5)
+    parts = []
+    for s in plan_slabs(dims, 2):
+        codes, ov, oi = oracle.lorenzo_c(data[s.offset:s.offset + s.count], s.dims, 1e-4)
+        book, rv = oracle.codebook(oracle.histogram(codes))  # per-slab books: not mergeable
+        parts.append(oracle_archive(oracle, codes, ov, oi, s.dims, 1e-4, book, rv, sublen=256))
+    with pytest.raises(cz.PszError):
+        cz.merge_archives(parts, dims)
