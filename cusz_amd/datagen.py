@@ -69,25 +69,37 @@ def hacc1d_torch(n, seed=3, jump=0.05, device="cuda"):
     return out
 
 
-def nyx_fields_torch(dims, seeds=range(10, 16), device="cuda"):
-    """config 4: six Nyx-like fields (log-normal density, 3 velocities, temperature)."""
+def nyx_fields_torch(dims, seeds=range(10, 16), device="cuda", z0=0, z1=None):
+    """config 4: six Nyx-like fields -- log-normal density exp(0.5 G), three
+    velocities 200 G, temperature 1e4 exp(0.3 G), a sixth log-normal -- where G is a smooth
+    field (32 seeded plane waves) + 1e-3 noise.  Planes [z0, z1) only (a rank's slab); the noise
+    of plane z comes from its own generator, so a slab equals the same planes of the whole field."""
     import torch
 
     x, y, z = dims
+    z1 = z if z1 is None else z1
     out = []
+    xs = torch.arange(x, device=device, dtype=torch.float64)
+    ys = torch.arange(y, device=device, dtype=torch.float64)
     for i, s in enumerate(seeds):
         g = torch.Generator(device=device)
         g.manual_seed(s)
         k = torch.rand((32, 3), generator=g, device=device, dtype=torch.float64) * 0.2
         ph = torch.rand(32, generator=g, device=device, dtype=torch.float64) * 6.283
-        xs = torch.arange(x, device=device, dtype=torch.float64)
-        ys = torch.arange(y, device=device, dtype=torch.float64)
-        f = torch.empty(z * y * x, device=device, dtype=torch.float32)
-        for zi in range(z):
-            G = torch.zeros((y, x), device=device, dtype=torch.float64)
+        f = torch.empty((z1 - z0) * y * x, device=device, dtype=torch.float32)
+        step = 16
+        for c0 in range(z0, z1, step):
+            c1 = min(z1, c0 + step)
+            zs = torch.arange(c0, c1, device=device, dtype=torch.float64)
+            G = torch.zeros((c1 - c0, y, x), device=device, dtype=torch.float64)
             for j in range(32):
-                G += torch.sin(k[j, 0] * xs[None, :] + k[j, 1] * ys[:, None] + k[j, 2] * zi + ph[j])
-            G = G / 4.0 + 1e-3 * torch.randn((y, x), generator=g, device=device, dtype=torch.float64)
+                G += torch.sin(k[j, 0] * xs[None, None, :] + k[j, 1] * ys[None, :, None] + k[j, 2] * zs[:, None, None]
+                               + ph[j])
+            G /= 4.0
+            for zi in range(c0, c1):
+                gn = torch.Generator(device=device)
+                gn.manual_seed(s * 100003 + zi)
+                G[zi - c0] += 1e-3 * torch.randn((y, x), generator=gn, device=device, dtype=torch.float64)
             if i == 0:
                 v = torch.exp(0.5 * G)
             elif i < 4:
@@ -96,6 +108,6 @@ def nyx_fields_torch(dims, seeds=range(10, 16), device="cuda"):
                 v = 1e4 * torch.exp(0.3 * G)
             else:
                 v = torch.exp(0.5 * G) * 0.1
-            f[zi * x * y:(zi + 1) * x * y] = v.reshape(-1).to(torch.float32)
+            f[(c0 - z0) * x * y:(c1 - z0) * x * y] = v.reshape(-1).to(torch.float32)
         out.append(f)
     return out

@@ -99,18 +99,30 @@ def allreduce_histograms(hists, dist):
     return hists
 
 
-def compress_fields_sharded(resources, d_ptrs, eb, dist, mode=0, radius=512, device=None):
-    """Sharded compress of several fields whose slabs this rank holds, with one codebook per
-    field shared by all ranks: pass 1 per slab, ONE all-reduce of the [fields, bklen]
-    histograms, then finish every slab.  Returns [(archive_ptr, nbytes)] (device archives,
-    valid until the manager's next compress)."""
+def global_value_ranges(fields, dist):
+    """Rel (r2r) mode across slabs: max - min of every field over all ranks (one all-reduce of
+    [fields, 2]; libcusz.cc:287-293 computes this range per field on one GPU)."""
+    import torch
+
+    mm = torch.stack([torch.stack([-a.double(), b.double()]) for a, b in (torch.aminmax(f) for f in fields)])
+    dist.all_reduce(mm, op=dist.ReduceOp.MAX)
+    return [float(hi + lo) for lo, hi in mm.tolist()]
+
+
+def compress_fields_sharded(resources, fields, eb, dist, mode=0, radius=512, device=None):
+    """Sharded compress of several fields whose slabs (device tensors `fields`) this rank holds,
+    with one codebook per field shared by all ranks: pass 1 per slab, ONE all-reduce of the
+    [fields, bklen] histograms, then finish every slab.  Rel mode: eb times the field's global
+    value range (one more all-reduce), the slabs then compress with that absolute bound.
+    Returns [(archive_ptr, nbytes)] (device archives, valid until the manager's next compress)."""
     import torch
 
     bklen = 2 * radius
     f = len(resources)
+    ebs = [eb * r for r in global_value_ranges(fields, dist)] if mode == 1 else [eb] * f
     h32 = torch.zeros((f, bklen), dtype=torch.int32, device=device)
-    for i, (r, p) in enumerate(zip(resources, d_ptrs)):
-        r.compress_scan(p, eb, h32[i].data_ptr(), mode, radius)
+    for i, (r, t) in enumerate(zip(resources, fields)):
+        r.compress_scan(t.data_ptr(), ebs[i], h32[i].data_ptr(), 0, radius)
     torch.cuda.synchronize(device)  # the scans run on the managers' streams
     h64 = h32.to(torch.int64)
     allreduce_histograms(h64, dist)
