@@ -381,7 +381,7 @@ pszerror psz_compress(psz_compressor* comp, void* d_in, psz_len3 const in_len3, 
   int s = comp->ctx->header->dtype == F4
               ? psz_compress_float(m, rc, (float*)d_in, header, d_compressed, comp_bytes)
               : psz_compress_double(m, rc, (double*)d_in, header, d_compressed, comp_bytes);
-  if (header) *comp->ctx->header = *header;
+  *comp->ctx->header = *m->header;  // psz_decompress reads it back (also when header == NULL)
   comp->last_error = (psz_error_status)s;
   return (pszerror)s;
 }

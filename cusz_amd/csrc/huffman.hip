@@ -23,20 +23,6 @@ namespace cusz_amd {
 
 namespace {
 
-constexpr int kEncThreads = 256;
-constexpr int kMaxGroup = 8;
-constexpr unsigned long long kFlagAgg = 1ull << 32;
-constexpr unsigned long long kFlagIncl = 2ull << 32;
-constexpr unsigned int kSpinLimit = 1u << 20;
-
-__device__ __forceinline__ unsigned long long ld_status(unsigned long long* p)
-{
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_status(unsigned long long* p, unsigned long long v)
-{
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // inclusive wave64 prefix sum with DPP (row_shr inside 16-lane rows, then row_bcast15/31 across
 // rows): six VALU ops instead of six LDS-routed ds_bpermute round trips
@@ -58,26 +44,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
   return v;
 }
 
-// exclusive scan over the 256-thread workgroup; returns the prefix, writes the total
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wave, uint32_t& total)
-{
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const uint32_t inc = wave_incl_scan(v, lane);
-  if (lane == 63) s_wave[wid] = inc;
-  __syncthreads();
-  uint32_t off = 0, tot = 0;
-#pragma unroll
-  for (int w = 0; w < kEncThreads / 64; w++) {
-    const uint32_t t = s_wave[w];
-    off += (w < wid) ? t : 0u;
-    tot += t;
-  }
-  __syncthreads();
-  total = tot;
-  return off + inc - v;
-}
 
-constexpr int kMaxPer = 32;  // sublen <= 8192
 
 // Pack this thread's codewords (MSB-first, starting at bit `pos` of the chunk) into the LDS
 // cell buffer.  Words that only this thread touches are plain stores; the first word (when
@@ -111,118 +78,8 @@ __device__ __forceinline__ void pack_words(uint32_t* cells, uint32_t pos, const 
   if (fill) atomicOr(&cells[q], (uint32_t)(acc >> 32));
 }
 
-__global__ void __launch_bounds__(kEncThreads) k_hf_encode(HfEncodeArgs a, int G, int cellcap)
-{
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t* s_book = smem;                    // bklen words
-  uint32_t* s_cells = smem + a.bklen;         // G * cellcap words
-  __shared__ uint32_t s_wave[kEncThreads / 64];
-  __shared__ uint32_t s_nbit[kMaxGroup];
-  __shared__ uint32_t s_base;
-
-  for (int i = threadIdx.x; i < a.bklen; i += kEncThreads) s_book[i] = a.book[i];
-  for (int i = threadIdx.x; i < G * cellcap; i += kEncThreads) s_cells[i] = 0;
-  __syncthreads();
-
-  const int g = blockIdx.x;
-  const int per = a.sublen / kEncThreads;
-  const int c0 = g * G;
-
-  for (int j = 0; j < G; j++) {
-    const int c = c0 + j;
-    if (c >= a.pardeg) {
-      if (threadIdx.x == 0) s_nbit[j] = 0;
-      continue;
-    }
-    const size_t start = (size_t)c * a.sublen;
-    const int cnt = (int)((a.n - start) < (size_t)a.sublen ? (a.n - start) : (size_t)a.sublen);
-    // this thread's codes [tid*per, tid*per + per) -> codewords in registers
-    const int lo = threadIdx.x * per;
-    const int mine = cnt - lo < 0 ? 0 : (cnt - lo < per ? cnt - lo : per);
-    const uint16_t* p = a.codes + start + lo;
-    uint32_t w[kMaxPer];
-    uint32_t bits = 0;
-    if ((per & 7) == 0 && mine == per) {
-#pragma unroll
-      for (int i = 0; i < kMaxPer; i += 8) {
-        if (i >= per) break;
-        const uint4 v = *reinterpret_cast<const uint4*>(p + i);
-        const uint32_t vs[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int h = 0; h < 4; h++) w[i + 2 * h] = s_book[vs[h] & 0xFFFFu], w[i + 2 * h + 1] = s_book[vs[h] >> 16];
-      }
-    }
-    else {
-#pragma unroll
-      for (int i = 0; i < kMaxPer; i++)
-        if (i < mine) w[i] = s_book[p[i]];
-    }
-#pragma unroll
-    for (int i = 0; i < kMaxPer; i++)
-      if (i < mine) bits += w[i] >> 27;
-    uint32_t total;
-    const uint32_t pos = block_excl_scan(bits, s_wave, total);
-    if (mine) pack_words(s_cells + j * cellcap, pos, w, mine);
-    if (threadIdx.x == 0) s_nbit[j] = total;
-  }
-  __syncthreads();
-
-  uint32_t gcells = 0;
-  for (int j = 0; j < G; j++) gcells += (s_nbit[j] + 31) >> 5;
-
-  // decoupled look-back over group status words
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    uint32_t base = 0;
-    if (g == 0) {
-      if (lane == 0) st_status(&a.status[0], kFlagIncl | gcells);
-    }
-    else {
-      if (lane == 0) st_status(&a.status[g], kFlagAgg | gcells);
-      int j = g - 1;
-      unsigned int spins = 0;
-      while (true) {
-        const int idx = j - lane;
-        const unsigned long long st = idx >= 0 ? ld_status(&a.status[idx]) : kFlagIncl;
-        const uint32_t flag = (uint32_t)(st >> 32);
-        if (__ballot(flag == 0)) {
-          if (++spins > kSpinLimit) {
-            if (lane == 0) atomicOr(a.timeout, 1u);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        const unsigned long long incl = __ballot(flag == 2);
-        const int first = incl ? (__ffsll((long long)incl) - 1) : 64;
-        base += wave_sum(lane <= first ? (uint32_t)st : 0u);
-        if (incl) break;
-        j -= 64;
-      }
-      if (lane == 0) st_status(&a.status[g], kFlagIncl | (unsigned long long)(base + gcells));
-    }
-    if (lane == 0) s_base = base;
-  }
-  __syncthreads();
-
-  uint32_t off = s_base;
-  for (int j = 0; j < G; j++) {
-    const int c = c0 + j;
-    if (c >= a.pardeg) break;
-    const uint32_t nb = s_nbit[j], nc = (nb + 31) >> 5;
-    if (threadIdx.x == 0) a.par_nbit[c] = nb, a.par_entry[c] = off;
-    const uint32_t* cells = s_cells + j * cellcap;
-    for (uint32_t i = threadIdx.x; i < nc; i += kEncThreads) a.bitstream[off + i] = cells[i];
-    off += nc;
-  }
-}
-
-// ---- wave-per-chunk encoder ------------------------------------------------------------------
-// Same output as k_hf_encode; each wave owns one chunk, so the bit offsets come from a wave
-// scan (no workgroup barrier per chunk) and the four chunks of a workgroup are packed
-// concurrently.  Codes are read 16 per lane per round (two 16-B loads, issued for the next
-// round before the current one is packed).  The workgroup's cell offset comes from the same
-// decoupled look-back.
+// codes are read 16 per lane per round (two 16-B loads, issued for the next round before the
+// current one is packed)
 constexpr int kEncW = 4;    // chunks (waves) per workgroup
 constexpr int kRound = 16;  // codes per lane per round
 
@@ -241,133 +98,10 @@ __device__ __forceinline__ void load_codes16(const uint16_t* p, int mine, uint32
   }
 }
 
-#ifdef CUSZ_AMD_DEC_PROFILE
-// per-workgroup encoder phase clocks (diagnostic build): setup, pack, look-back, write-out
-__device__ unsigned long long g_enc_prof[65536 * 4];
-#endif
 
-__global__ void __launch_bounds__(64 * kEncW) k_hf_encode_w(HfEncodeArgs a, int cellcap)
-{
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t* s_book = smem;                                  // bklen words (rounded to 4)
-  uint32_t* s_cells = smem + ((a.bklen + 3) & ~3);          // kEncW * cellcap words
-  __shared__ uint32_t s_nbit[kEncW];
-  __shared__ uint32_t s_base;
-
-#ifdef CUSZ_AMD_DEC_PROFILE
-  unsigned long long ept[5];
-  ept[0] = __builtin_readcyclecounter();
-#endif
-  for (int i = threadIdx.x; i < a.bklen; i += blockDim.x) s_book[i] = a.book[i];
-  for (int i = threadIdx.x; i < kEncW * cellcap / 4; i += blockDim.x)
-    reinterpret_cast<uint4*>(s_cells)[i] = make_uint4(0, 0, 0, 0);
-  __syncthreads();
-#ifdef CUSZ_AMD_DEC_PROFILE
-  ept[1] = __builtin_readcyclecounter();
-#endif
-
-  const int g = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int c = g * kEncW + wid;
-  uint32_t nbits = 0;
-  if (c < a.pardeg) {
-    const size_t start = (size_t)c * a.sublen;
-    const int cnt = (int)((a.n - start) < (size_t)a.sublen ? (a.n - start) : (size_t)a.sublen);
-    const int per = a.sublen / 64 < kRound ? a.sublen / 64 : kRound;  // codes per lane per round
-    const int span = per * 64;
-    uint32_t* cells = s_cells + wid * cellcap;
-    const uint16_t* src = a.codes + start;
-    const bool vec_ok = per == kRound;
-    uint32_t nxt[8];
-    {
-      const int lo = lane * per, mine = min(max(cnt - lo, 0), per);
-      load_codes16(src + lo, mine, nxt, vec_ok && mine == per);
-    }
-    for (int r0 = 0; r0 < cnt; r0 += span) {
-      const int lo = r0 + lane * per, mine = min(max(cnt - lo, 0), per);
-      uint32_t cur[8];
-#pragma unroll
-      for (int i = 0; i < 8; i++) cur[i] = nxt[i];
-      if (r0 + span < cnt) {  // prefetch the next round
-        const int lo2 = lo + span, mine2 = min(max(cnt - lo2, 0), per);
-        load_codes16(src + lo2, mine2, nxt, vec_ok && mine2 == per);
-      }
-      uint32_t w[kRound], bits = 0;
-#pragma unroll
-      for (int i = 0; i < kRound; i++) {
-        const uint32_t code = (cur[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
-        w[i] = i < mine ? s_book[code] : 0u;
-        bits += w[i] >> 27;
-      }
-      const uint32_t inc = wave_incl_scan(bits, lane);
-      if (mine) pack_words<kRound>(cells, nbits + inc - bits, w, mine);
-      nbits += __shfl(inc, 63);
-    }
-  }
-  if (lane == 0) s_nbit[wid] = nbits;
-  __syncthreads();
-#ifdef CUSZ_AMD_DEC_PROFILE
-  ept[2] = __builtin_readcyclecounter();
-#endif
-
-  uint32_t gcells = 0;
-  for (int j = 0; j < kEncW; j++) gcells += (s_nbit[j] + 31) >> 5;
-
-  // decoupled look-back over group status words
-  if (threadIdx.x < 64) {
-    uint32_t base = 0;
-    if (g == 0) {
-      if (lane == 0) st_status(&a.status[0], kFlagIncl | gcells);
-    }
-    else {
-      if (lane == 0) st_status(&a.status[g], kFlagAgg | gcells);
-      int j = g - 1;
-      unsigned int spins = 0;
-      while (true) {
-        const int idx = j - lane;
-        const unsigned long long st = idx >= 0 ? ld_status(&a.status[idx]) : kFlagIncl;
-        const uint32_t flag = (uint32_t)(st >> 32);
-        if (__ballot(flag == 0)) {
-          if (++spins > kSpinLimit) {
-            if (lane == 0) atomicOr(a.timeout, 1u);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        const unsigned long long incl = __ballot(flag == 2);
-        const int first = incl ? (__ffsll((long long)incl) - 1) : 64;
-        base += wave_sum(lane <= first ? (uint32_t)st : 0u);
-        if (incl) break;
-        j -= 64;
-      }
-      if (lane == 0) st_status(&a.status[g], kFlagIncl | (unsigned long long)(base + gcells));
-    }
-    if (lane == 0) s_base = base;
-  }
-  __syncthreads();
-#ifdef CUSZ_AMD_DEC_PROFILE
-  ept[3] = __builtin_readcyclecounter();
-#endif
-
-  // each wave writes its own chunk (cells start on a fresh cell per chunk)
-  uint32_t off = s_base;
-  for (int j = 0; j < wid; j++) off += (s_nbit[j] + 31) >> 5;
-  if (c < a.pardeg) {
-    const uint32_t nb = s_nbit[wid], nc = (nb + 31) >> 5;
-    if (lane == 0) a.par_nbit[c] = nb, a.par_entry[c] = off;
-    const uint32_t* cells = s_cells + wid * cellcap;
-    for (uint32_t i = lane; i < nc; i += 64) a.bitstream[off + i] = cells[i];
-  }
-#ifdef CUSZ_AMD_DEC_PROFILE
-  ept[4] = __builtin_readcyclecounter();
-  if (threadIdx.x == 0 && g < 65536)
-    for (int q = 0; q < 4; q++) g_enc_prof[g * 4 + q] = ept[q + 1] - ept[q];
-#endif
-}
-
-// ---- three-phase encoder (default) ------------------------------------------------------------
-// The look-back encoders above serialise workgroups on their predecessors' prefixes; on MI355X
-// that latency, not bandwidth, bounds them.  Here:
+// ---- three-phase encoder (reference layout) ----------------------------------------------------
+// A decoupled look-back serialises workgroups on their predecessors' prefixes; on MI355X that
+// latency, not bandwidth, bounds it (measured in round 1).  Here:
 //  (1) k_hf_pack: persistent waves, one chunk per wave at a time, codes prefetched a round
 //      ahead; the chunk's cells go to a scratch slot at a fixed worst-case stride;
 //  (2) k_hf_chunk_scan: one workgroup scans the per-chunk cell counts into par_entry;
@@ -719,160 +453,7 @@ struct DecProf {
 #endif
 };
 
-// ---- lane-per-chunk decoder (the reference's decomposition, hf_kernels.cuhip.inl:331-396) ----
-// Each lane decodes one whole chunk, so there is no synchronisation pass and every codeword is
-// decoded once.  Per lane: a 4-block (16-cell) LDS ring fed by 16-B loads issued two cadences
-// ahead (two alternating register slots, so the wait for one never waits for the other), and
-// a 32-symbol LDS output ring flushed in 32-B stores.  Steps are taken in cadences of kCad
-// (uniform across the wave) so refills and flushes happen at wave-uniform points.
-constexpr int kLpcThreads = 256;
-constexpr int kInStride = 20;   // words per lane: 16 ring cells + pad (16-B aligned, staggers banks)
-constexpr int kOutStride = 20;  // words per lane: 32 symbols + pad
 constexpr int kCad = 4;         // <= 4 * 27 bits consumed per cadence < one 128-bit block
-
-__global__ void __launch_bounds__(kLpcThreads) k_hf_decode_lane(HfDecodeArgs a)
-{
-  __shared__ __attribute__((aligned(16))) uint32_t s_l1[kL1];
-  __shared__ __attribute__((aligned(16))) uint32_t s_l2[kL2Cap];
-  __shared__ uint32_t s_base[32];
-  __shared__ uint16_t s_keys[kMaxBklen];
-  __shared__ __attribute__((aligned(16))) uint32_t s_in[kLpcThreads * kInStride];
-  __shared__ __attribute__((aligned(16))) uint32_t s_out[kLpcThreads * kOutStride];
-  HfTables tb;
-  load_tables(a, s_l1, s_l2, s_base, s_keys, tb);
-
-  const uint32_t c = blockIdx.x * kLpcThreads + threadIdx.x;
-  const size_t obase = (size_t)c * a.sublen;
-  const bool live = c < (uint32_t)a.pardeg && obase < a.n;
-  const uint32_t nsym = live ? (uint32_t)min((size_t)a.sublen, a.n - obase) : 0u;
-  const uint32_t nbit = live ? a.par_nbit[c] : 0u;
-  const uint32_t entry = live ? a.par_entry[c] : 0u;
-  const uint32_t ncell = (nbit + 31) >> 5;
-  // 16-B aligned view of this chunk's cells: block b = bytes [16b, 16b+16) from `gb`
-  const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(a.bitstream + entry) & 15);
-  const uint4* gb = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.bitstream + entry) - mis);
-  const uint32_t skip = mis >> 2;
-  const uint32_t nblk = (skip + ncell + 3) >> 2;
-  const bool tail = live && c + 1 == (uint32_t)a.pardeg;  // last chunk: never read past its cells
-  // Every cadence issues exactly one 16-B load and two 16-B stores per lane, unconditionally
-  // (targets swapped for safe dummies when unused), so the compiler's vmcnt waits are exact
-  // and a ring refill waits only for its own load, issued two cadences earlier.  The last
-  // chunk's final partial block is read once, by cells, before the loop (never past the end).
-  const uint4* gsafe = reinterpret_cast<const uint4*>(a.lut);
-  const uint32_t tb_blk = nblk ? nblk - 1 : 0u;  // the last block of this chunk
-  const bool tail_partial = tail && nblk && (tb_blk + 1) * 4 > skip + ncell;
-  uint4 tailv = make_uint4(0, 0, 0, 0);
-  if (tail_partial) {
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(gb + tb_blk);
-    const uint32_t lim = skip + ncell - tb_blk * 4;  // valid cells in this block (1..3)
-    tailv.x = q[0];
-    tailv.y = lim > 1 ? q[1] : 0u;
-    tailv.z = lim > 2 ? q[2] : 0u;
-  }
-  // raw 16-B load of block b (the tail block's stand-in is substituted when it is written to
-  // the ring, so the loaded registers are not touched before the ring write needs them)
-  auto load_block = [&](uint32_t b) -> uint4 {
-    const uint32_t bb = min(b, tb_blk);
-    const bool use_tail = tail_partial && bb == tb_blk;
-    return *((live && !use_tail) ? gb + bb : gsafe);
-  };
-  uint32_t* ring = s_in + threadIdx.x * kInStride;
-  uint16_t* oring = reinterpret_cast<uint16_t*>(s_out + threadIdx.x * kOutStride);
-  auto ring_put = [&](uint32_t b, uint4 v) {
-    if (tail_partial && b == tb_blk) v = tailv;
-    reinterpret_cast<uint4*>(ring)[b & 3] = v;
-  };
-
-  // prologue: up to 4 blocks into the ring, two more in flight
-  uint32_t ld = min(nblk, 4u);
-  {
-    uint4 v[4];
-#pragma unroll
-    for (int b = 0; b < 4; b++) v[b] = load_block(b);
-#pragma unroll
-    for (int b = 0; b < 4; b++)
-      if ((uint32_t)b < ld) ring_put(b, v[b]);
-  }
-  uint32_t bA = ld, bB = ld + 1;
-  uint32_t cnt = 0, flushed = 0;
-  uint16_t* gout = a.out + obase;
-  // bit buffer: the next `avail` (>= 32 before every step) stream bits, MSB-aligned; `nxt` is
-  // cell `nw`, read from the ring one refill ahead so the refill never waits on LDS
-  uint64_t buf = ((uint64_t)ring[skip & 15] << 32) | ring[(skip + 1) & 15];
-  uint32_t avail = 64, nw = skip + 2;
-  uint32_t nxt = ring[nw & 15];
-
-  // flush 16 symbols (32 B) when a ring half is full (scattered per-lane stores are costly
-  // in the address path, so they are issued only when there is something to write)
-  auto flush = [&]() {
-    if (cnt - flushed >= 16u) {
-      const uint4* src = reinterpret_cast<const uint4*>(oring + (flushed & 16u));
-      uint4* dst = reinterpret_cast<uint4*>(gout + flushed);
-      const uint4 v0 = src[0], v1 = src[1];
-      dst[0] = v0;
-      dst[1] = v1;
-      flushed += 16;
-    }
-  };
-  auto steps = [&]() {
-#pragma unroll
-    for (int s = 0; s < kCad; s++) {
-      // a lane whose ring has not caught up (never in steady state) skips the step
-      if (cnt < nsym && (nw + 1 < ld * 4 || ld >= nblk)) {
-        const uint32_t e = hf_entry(tb, (uint32_t)(buf >> 32));
-        const uint32_t l0 = (e >> 20) & 31u;
-        const bool both = (e >> 30) == 2u && cnt + 1 < nsym;
-        const uint32_t i0 = cnt & 31u, i1 = both ? ((cnt + 1) & 31u) : i0;
-        oring[i0] = (uint16_t)(e & 1023u);
-        oring[i1] = (uint16_t)(both ? ((e >> 10) & 1023u) : (e & 1023u));
-        cnt += both ? 2u : 1u;
-        const uint32_t l = both ? ((e >> 25) & 31u) : l0;
-        buf <<= l;
-        avail -= l;
-        if (avail < 32) {
-          buf |= (uint64_t)nxt << (32 - avail);
-          avail += 32;
-          nw++;
-          nxt = ring[nw & 15];
-        }
-      }
-    }
-  };
-  auto cadence = [&](uint4& p, uint32_t& b) {
-    if (b == ld && ld < nblk && ld - (nw >> 2) < 4u) {
-      ring_put(ld, p);
-      ld++;
-    }
-    if (b < ld) b += 2;
-    flush();
-    p = load_block(b);
-  };
-  uint4 pA = load_block(bA), pB = load_block(bB);
-  DecProf pf;
-  pf.start();
-  uint32_t iters = 0;
-  while (__any(cnt < nsym)) {
-    steps();
-    pf.mark(1);
-    cadence(pA, bA);
-    pf.mark(2);
-    steps();
-    pf.mark(1);
-    cadence(pB, bB);
-    pf.mark(2);
-    iters++;
-  }
-  wave_sync();
-  for (uint32_t i = flushed; i < cnt; i++) gout[i] = oring[i & 31u];
-  pf.mark(4);
-  pf.add(8, iters);
-  pf.add(13, 1u);
-#ifdef CUSZ_AMD_DEC_PROFILE
-  const unsigned gw = (blockIdx.x * kLpcThreads + threadIdx.x) >> 6;
-  if ((threadIdx.x & 63) == 0 && gw < 4096)
-    for (int k = 0; k < 16; k++) g_dec_prof[gw * 16 + k] = pf.v[k];
-#endif
-}
 
 // ---- windowed lane-per-chunk decoder ------------------------------------------------------------
 // Each lane decodes one whole chunk (every codeword decoded once).  The workgroup's 512 chunks
@@ -1072,209 +653,6 @@ __global__ void __launch_bounds__(kWinLanes) k_hf_decode_win(HfDecodeArgs a)
 #undef CUSZ_STAGE_STORE
 }
 
-// ---- register-pack lane-per-chunk decoder --------------------------------------------------------
-// One lane per chunk.  The lane keeps the last 8 output symbols in a 4-register shift pack
-// (v_perm_b32 pushes one or two symbols per table step); a two-symbol step never straddles an
-// aligned group of 8 output positions, so the pack completes exactly on group boundaries.  A
-// completed group goes to the lane's 128-B LDS stage with one ds_write_b128; at cadence points a
-// lane whose stage holds a whole 32-symbol block writes it out as 64 contiguous bytes (4 x 16-B
-// stores back to back), so the memory side sees full 64-B segments instead of scattered 16-B
-// pieces (those cost more than the decode itself: measured 630 vs 270 us at 512^3).  The only
-// other LDS traffic of a step is the table lookup and, every ~4 steps, the next input cell from
-// the lane's 16-cell ring.  Partial groups/blocks at unaligned chunk ends use narrower stores.
-constexpr int kPkThreads = 512;
-constexpr int kPkStride = 20;   // input ring words per lane (16 cells, 16-B aligned, banks staggered)
-constexpr int kPkStage = 36;    // stage words per lane (8 groups of 16 B + pad: b128 banks disjoint)
-constexpr uint32_t kSel1 = 0x05040302u;  // v_perm selector: shift the pack by one symbol
-constexpr uint32_t kSel2 = 0x07060504u;  // ... by two symbols
-
-struct Pack8 {
-  uint32_t p0, p1, p2, p3;  // slot j = bits 16(j&1) of p[j>>1]; slot 7 is the newest
-  __device__ __forceinline__ void push(uint32_t s, uint32_t sel)
-  {
-    p0 = __builtin_amdgcn_perm(p1, p0, sel);
-    p1 = __builtin_amdgcn_perm(p2, p1, sel);
-    p2 = __builtin_amdgcn_perm(p3, p2, sel);
-    p3 = __builtin_amdgcn_perm(s, p3, sel);
-  }
-  __device__ __forceinline__ uint16_t slot(int j) const
-  {
-    const uint32_t w = j < 2 ? p0 : j < 4 ? p1 : j < 6 ? p2 : p3;
-    return (uint16_t)(w >> (16 * (j & 1)));
-  }
-};
-
-template <int MODE>  // 0: staged 64-B flushes; 1 (diagnostic): no output; 2 (diagnostic): direct 16-B stores
-__global__ void __launch_bounds__(kPkThreads) k_hf_decode_pk(HfDecodeArgs a)
-{
-  __shared__ __attribute__((aligned(16))) uint32_t s_l1[kL1];
-  __shared__ __attribute__((aligned(16))) uint32_t s_l2[kL2Cap];
-  __shared__ uint32_t s_base[32];
-  __shared__ uint16_t s_keys[kMaxBklen];
-  __shared__ __attribute__((aligned(16))) uint32_t s_in[kPkThreads * kPkStride];
-  __shared__ __attribute__((aligned(16))) uint32_t s_stage[MODE == 0 ? kPkThreads * kPkStage : 4];
-  __shared__ uint32_t s_reqA[kPkThreads / 64][64];
-  __shared__ uint8_t s_reqL[kPkThreads / 64][64];
-  HfTables tb;
-  load_tables(a, s_l1, s_l2, s_base, s_keys, tb);
-
-  const uint32_t c = blockIdx.x * kPkThreads + threadIdx.x;
-  const size_t obase = (size_t)c * a.sublen;
-  const bool live = c < (uint32_t)a.pardeg && obase < a.n;
-  const uint32_t nsym = live ? (uint32_t)min((size_t)a.sublen, a.n - obase) : 0u;
-  const uint32_t nbit = live ? a.par_nbit[c] : 0u;
-  const uint32_t entry = live ? a.par_entry[c] : 0u;
-  const uint32_t ncell = (nbit + 31) >> 5;
-  const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(a.bitstream + entry) & 15);
-  const uint4* gb = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.bitstream + entry) - mis);
-  const uint32_t skip = mis >> 2;
-  const uint32_t nblk = (skip + ncell + 3) >> 2;
-  const bool tail = live && c + 1 == (uint32_t)a.pardeg;
-  const uint4* gsafe = reinterpret_cast<const uint4*>(a.lut);
-  const uint32_t tb_blk = nblk ? nblk - 1 : 0u;
-  const bool tail_partial = tail && nblk && (tb_blk + 1) * 4 > skip + ncell;
-  uint4 tailv = make_uint4(0, 0, 0, 0);
-  if (tail_partial) {
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(gb + tb_blk);
-    const uint32_t lim = skip + ncell - tb_blk * 4;
-    tailv.x = q[0];
-    tailv.y = lim > 1 ? q[1] : 0u;
-    tailv.z = lim > 2 ? q[2] : 0u;
-  }
-  auto load_block = [&](uint32_t b) -> uint4 {
-    const uint32_t bb = min(b, tb_blk);
-    const bool use_tail = tail_partial && bb == tb_blk;
-    return *((live && !use_tail) ? gb + bb : gsafe);
-  };
-  uint32_t* ring = s_in + threadIdx.x * kPkStride;
-  auto ring_put = [&](uint32_t b, uint4 v) {
-    if (tail_partial && b == tb_blk) v = tailv;
-    reinterpret_cast<uint4*>(ring)[b & 3] = v;
-  };
-  uint32_t ld = min(nblk, 4u);
-  {
-    uint4 v[4];
-#pragma unroll
-    for (int b = 0; b < 4; b++) v[b] = load_block(b);
-#pragma unroll
-    for (int b = 0; b < 4; b++)
-      if ((uint32_t)b < ld) ring_put(b, v[b]);
-  }
-  uint32_t bA = ld, bB = ld + 1;
-  uint64_t buf = ((uint64_t)ring[skip & 15] << 32) | ring[(skip + 1) & 15];
-  uint32_t avail = 64, nw = skip + 2;
-  uint32_t nxt = ring[nw & 15];
-
-  // output: absolute index A of the next symbol; groups of 8 are aligned on absolute indices
-  const uint32_t A0 = (uint32_t)obase;
-  const uint32_t Aend = A0 + nsym;
-  const uint32_t Afirst = (A0 + 31) & ~31u;  // first 32-block boundary; earlier groups go direct
-  uint32_t A = A0, Aflushed = Afirst;       // staged blocks flushed up to Aflushed
-  Pack8 pk{0, 0, 0, 0};
-  char* outb = reinterpret_cast<char*>(a.out);
-  uint4* stage = reinterpret_cast<uint4*>(s_stage + (MODE == 0 ? threadIdx.x * kPkStage : 0));
-  auto store_group = [&](uint32_t g0) {  // the pack = positions [g0, g0+8), clipped to [A0, Aend)
-    if (g0 >= A0 && g0 + 8 <= Aend) {
-      *reinterpret_cast<uint4*>(outb + 2 * (size_t)g0) = make_uint4(pk.p0, pk.p1, pk.p2, pk.p3);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const uint32_t pos = g0 + j;
-        if (pos >= A0 && pos < Aend) *reinterpret_cast<uint16_t*>(outb + 2 * (size_t)pos) = pk.slot(j);
-      }
-    }
-  };
-  // Cooperative flush (wave-uniform call): every lane whose stage holds a whole 32-symbol block
-  // posts it; four lanes write each posted block, so a store instruction writes 16 contiguous
-  // 64-B pieces instead of 64 scattered 16-B ones (the address path handles one segment per cycle).
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  auto flush = [&]() {
-    const bool ready = A >= Aflushed + 32;
-    const uint64_t m = __ballot(ready);
-    if (!m) return;
-    // at most 32 blocks per call (two store instructions, so the compiler's vmcnt bookkeeping
-    // stays exact across the loop); a lane produces <= 8 symbols per cadence, so a block waits
-    // at most one extra call and the 8-group stage never wraps onto an unflushed group
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-    if (ready && rank < 32) {
-      s_reqA[wid][rank] = Aflushed;
-      s_reqL[wid][rank] = (uint8_t)lane;
-      Aflushed += 32;
-    }
-    wave_sync();
-    const uint32_t n = min((uint32_t)__popcll(m), 32u);
-#pragma unroll
-    for (uint32_t i0 = 0; i0 < 32; i0 += 16) {
-      const uint32_t i = i0 + (lane >> 2), j = lane & 3;
-      if (i < n) {
-        const uint32_t Af = s_reqA[wid][i];
-        const uint4* st = reinterpret_cast<const uint4*>(s_stage + (wid * 64 + s_reqL[wid][i]) * kPkStage);
-        const uint4 v = st[((Af >> 3) & 4u) + j];
-        *reinterpret_cast<uint4*>(outb + 2 * (size_t)Af + 16 * j) = v;
-      }
-    }
-    wave_sync();
-  };
-
-  auto steps = [&]() {
-#pragma unroll
-    for (int s = 0; s < kCad; s++) {
-      if (A < Aend) {
-        const uint32_t e = hf_entry(tb, (uint32_t)(buf >> 32));
-        const bool both = (e >> 31) && ((A & 7u) != 7u) && (A + 1 < Aend);
-        const uint32_t l = both ? ((e >> 25) & 31u) : ((e >> 20) & 31u);
-        const uint32_t S = (e & 1023u) | ((e << 6) & (1023u << 16));
-        pk.push(S, both ? kSel2 : kSel1);
-        A += both ? 2u : 1u;
-        buf <<= l;
-        avail -= l;
-        if (avail < 32) {
-          buf |= (uint64_t)nxt << (32 - avail);
-          avail += 32;
-          nw++;
-          nxt = ring[nw & 15];
-        }
-        if (MODE != 1 && !(A & 7u)) {
-          if (MODE == 0 && A - 8 >= Afirst)
-            stage[((A - 8) >> 3) & 7u] = make_uint4(pk.p0, pk.p1, pk.p2, pk.p3);
-          else
-            store_group(A - 8);
-        }
-      }
-    }
-  };
-  auto cadence = [&](uint4& p, uint32_t& b) {
-    if (b == ld && ld < nblk && ld - (nw >> 2) < 4u) {
-      ring_put(ld, p);
-      ld++;
-    }
-    if (MODE == 0) flush();
-    if (b < ld) {  // the block went into the ring: fetch the next one of this slot's parity
-      b += 2;
-      p = load_block(b);
-    }
-  };
-  uint4 pA = load_block(bA), pB = load_block(bB);
-  while (__any(A < Aend)) {
-    steps();
-    cadence(pA, bA);
-    steps();
-    cadence(pB, bB);
-  }
-  if (MODE == 0) {
-    while (__any(A >= Aflushed + 32)) flush();
-    // staged groups of an incomplete last block, then the partial last group
-    for (uint32_t g0 = Aflushed; g0 + 8 <= (Aend & ~7u); g0 += 8)
-      *reinterpret_cast<uint4*>(outb + 2 * (size_t)g0) = stage[(g0 >> 3) & 7u];
-  }
-  if (MODE != 1 && live && (Aend & 7u)) {
-    const uint32_t t = Aend & 7u;
-#pragma unroll
-    for (int k = 0; k < 7; k++)
-      if ((uint32_t)k < 8 - t) pk.push(0u, kSel1);
-    store_group(Aend & ~7u);
-  }
-}
 
 // ---- wave-per-chunk decoder (for few, long chunks) ------------------------------------------
 constexpr int kDecWaves = 4;   // waves per decode workgroup
@@ -1461,72 +839,42 @@ __global__ void __launch_bounds__(64 * kDecWaves) k_hf_decode(HfDecodeArgs a, in
 
 }  // namespace
 
-static int enc_group(int sublen, int& cellcap)
-{
-  cellcap = sublen * kLmax / 32 + 2;
-  int G = 32768 / (cellcap * 4);
-  if (G < 1) G = 1;
-  if (G > kMaxGroup) G = kMaxGroup;
-  return G;
-}
-
-static bool enc_wave(int sublen) { return sublen % 64 == 0; }
-
 static int enc_wave_cellcap(int sublen) { return ((sublen * kLmax / 32 + 2) + 3) / 4 * 4; }
 
 int hf_encode_groups(int sublen, int pardeg)
 {
-  if (enc_wave(sublen)) return (pardeg + kEncW - 1) / kEncW;
-  int cellcap;
-  const int G = enc_group(sublen, cellcap);
-  return (pardeg + G - 1) / G;
+  (void)sublen;
+  return (pardeg + kEncW - 1) / kEncW;
 }
 
 static size_t hf_encode_tile_words(int pardeg) { return ((size_t)pardeg + kGatherTile - 1) / kGatherTile + 4; }
 
 size_t hf_encode_temp_words(int sublen, int pardeg)
 {  // chunk slots at a worst-case stride, then the per-tile cell totals
-  return enc_wave(sublen) ? (size_t)enc_wave_cellcap(sublen) * (size_t)pardeg + hf_encode_tile_words(pardeg) : 0;
+  return (size_t)enc_wave_cellcap(sublen) * (size_t)pardeg + hf_encode_tile_words(pardeg);
 }
 
+// sublen: a multiple of 256 (the pipeline rounds it), so every chunk is a whole number of
+// 16-code lane rounds of its wave
 int launch_hf_encode(const HfEncodeArgs& a, hipStream_t st)
 {
-  if (a.temp && enc_wave(a.sublen)) {
-    const int cellcap = enc_wave_cellcap(a.sublen);
-    const size_t lds = (size_t)(((a.bklen + 3) & ~3) + kPackWaves * cellcap) * 4;
-    static int per_cu = 0, ncu = 0;
-    static size_t last_lds = 0;
-    if (lds != last_lds) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_hf_pack, 64 * kPackWaves, lds) != hipSuccess ||
-          per_cu < 1)
-        per_cu = 1;
-      last_lds = lds;
-    }
-    const int need = (a.pardeg + kPackWaves - 1) / kPackWaves;
-    const int grid = need < per_cu * ncu ? need : per_cu * ncu;
-    k_hf_pack<<<grid, 64 * kPackWaves, lds, st>>>(a, cellcap);
-    const int ntiles = (a.pardeg + kGatherTile - 1) / kGatherTile;
-    uint32_t* tile_sum = a.temp + hf_encode_temp_words(a.sublen, a.pardeg) - hf_encode_tile_words(a.pardeg);
-    k_hf_tile_sums<<<(ntiles + 3) / 4, 256, 0, st>>>(a.par_nbit, a.pardeg, tile_sum, ntiles);
-    k_hf_tile_scan<<<1, 1024, 0, st>>>(tile_sum, ntiles);
-    k_hf_gather<<<ntiles, 256, 0, st>>>(a, cellcap, tile_sum);
-    return (int)hipGetLastError();
-  }
-  if (enc_wave(a.sublen)) {
-    const int cellcap = enc_wave_cellcap(a.sublen);
-    const int ngroups = (a.pardeg + kEncW - 1) / kEncW;
-    const size_t lds = (size_t)(((a.bklen + 3) & ~3) + kEncW * cellcap) * 4;
-    k_hf_encode_w<<<ngroups, 64 * kEncW, lds, st>>>(a, cellcap);
-    return (int)hipGetLastError();
-  }
-  int cellcap;
-  const int G = enc_group(a.sublen, cellcap);
-  const int ngroups = (a.pardeg + G - 1) / G;
-  const size_t lds = (size_t)(a.bklen + G * cellcap) * 4;
-  k_hf_encode<<<ngroups, kEncThreads, lds, st>>>(a, G, cellcap);
+  if (!a.temp || a.sublen % 64 != 0 || a.sublen > 8192) return (int)hipErrorInvalidValue;
+  const int cellcap = enc_wave_cellcap(a.sublen);
+  const size_t lds = (size_t)(((a.bklen + 3) & ~3) + kPackWaves * cellcap) * 4;
+  int dev = 0, ncu = 0, per_cu = 0;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_hf_pack, 64 * kPackWaves, lds) != hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
+  const int need = (a.pardeg + kPackWaves - 1) / kPackWaves;
+  const int grid = need < per_cu * ncu ? need : per_cu * ncu;
+  k_hf_pack<<<grid, 64 * kPackWaves, lds, st>>>(a, cellcap);
+  const int ntiles = (a.pardeg + kGatherTile - 1) / kGatherTile;
+  uint32_t* tile_sum = a.temp + hf_encode_temp_words(a.sublen, a.pardeg) - hf_encode_tile_words(a.pardeg);
+  k_hf_tile_sums<<<(ntiles + 3) / 4, 256, 0, st>>>(a.par_nbit, a.pardeg, tile_sum, ntiles);
+  k_hf_tile_scan<<<1, 1024, 0, st>>>(tile_sum, ntiles);
+  k_hf_gather<<<ntiles, 256, 0, st>>>(a, cellcap, tile_sum);
   return (int)hipGetLastError();
 }
 
@@ -1535,23 +883,12 @@ int launch_hf_decode(const HfDecodeArgs& a, hipStream_t st)
   if (a.bklen < 1 || a.bklen > kMaxBklen || a.sublen < 1) return (int)hipErrorInvalidValue;
   k_hf_tables<<<1, 1024, 0, st>>>(a.revbook, a.bklen, a.lut);
   if (a.pardeg <= 0) return (int)hipGetLastError();
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
-  }
+  // the current device's CU count (queried per launch: one process may drive several GPUs)
+  int dev = 0, ncu = 0;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
   // Many chunks: one lane per chunk (every codeword decoded once).  Few long chunks: one wave
   // per chunk (three passes, but 64-way parallel inside a chunk).
-  if (a.decoder == 4 || a.decoder == 5) {
-    if (a.decoder == 4) k_hf_decode_pk<1><<<(a.pardeg + kPkThreads - 1) / kPkThreads, kPkThreads, 0, st>>>(a);
-    else k_hf_decode_pk<2><<<(a.pardeg + kPkThreads - 1) / kPkThreads, kPkThreads, 0, st>>>(a);
-    return (int)hipGetLastError();
-  }
-  if (a.decoder == 3) {
-    k_hf_decode_pk<0><<<(a.pardeg + kPkThreads - 1) / kPkThreads, kPkThreads, 0, st>>>(a);
-    return (int)hipGetLastError();
-  }
   const bool lane = a.sublen % 16 == 0 && (a.decoder == 1 || (a.decoder == 0 && a.pardeg >= 64 * ncu));
   if (lane) {
     k_hf_decode_win<<<(a.pardeg + kWinLanes - 1) / kWinLanes, kWinLanes, 0, st>>>(a);
@@ -1566,16 +903,17 @@ int launch_hf_decode(const HfDecodeArgs& a, hipStream_t st)
     cellcap = (int)((want + 15) / 16 * 16);
     if (cellcap > worst) cellcap = worst;
   }
-  const size_t lds = ((size_t)cellcap + (((size_t)a.sublen + 1) / 2 + 3) / 4 * 4) * 4 * kDecWaves;
-  if (lds > 120 * 1024) return (int)hipErrorInvalidValue;
-  static int per_cu = 0;
-  static size_t last_lds = 0;
-  if (lds != last_lds) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_hf_decode, 64 * kDecWaves, lds) != hipSuccess ||
-        per_cu < 1)
-      per_cu = 1;
-    last_lds = lds;
-  }
+  // the staging area never needs to cover a whole chunk (longer chunks decode from global
+  // memory): clamp it to the LDS left after the output tiles
+  const size_t tile_words = (((size_t)a.sublen + 1) / 2 + 3) / 4 * 4;
+  const size_t budget = 120 * 1024 / 4 / kDecWaves;
+  if (tile_words + 16 > budget) return (int)hipErrorInvalidValue;  // sublen > ~15k: never produced
+  if ((size_t)cellcap + tile_words > budget) cellcap = (int)((budget - tile_words) / 16 * 16);
+  const size_t lds = ((size_t)cellcap + tile_words) * 4 * kDecWaves;
+  int per_cu = 0;  // occupancy for this LDS size on the current device (no process-global cache)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_hf_decode, 64 * kDecWaves, lds) != hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
   const int nblk = (a.pardeg + kDecWaves - 1) / kDecWaves;
   const int full = per_cu * ncu;
   const int grid = nblk < full ? nblk : full;
@@ -1584,13 +922,6 @@ int launch_hf_decode(const HfDecodeArgs& a, hipStream_t st)
 }
 
 #ifdef CUSZ_AMD_DEC_PROFILE
-extern "C" int psz_amd_debug_encode_profile(unsigned long long* host, int nwords)
-{
-  if (nwords > 65536 * 4) nwords = 65536 * 4;
-  (void)hipDeviceSynchronize();
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_enc_prof), (size_t)nwords * 8, 0, hipMemcpyDeviceToHost);
-}
-
 // copies the per-wave decoder profile of the last decode (u64[4096*16]) to host memory
 extern "C" int psz_amd_debug_decode_profile(unsigned long long* host, int nwords)
 {

@@ -861,8 +861,13 @@ template <typename T>
 static int decompress_impl(psz_resource* m, uint8_t* in, size_t in_len, T* out)
 {
   if (!m || !in || !out) return PSZ_ABORT_NOT_IMPLEMENTED;
-  (void)in_len;
   Pipeline* p = cusz_amd::P(m);
+  // the header's segment table must be ordered and fit the archive the caller passed
+  const uint32_t* e = m->header->entry;
+  for (int k = 1; k <= PSZHEADER_ENC_PASS2_END; k++)
+    if (e[k] < e[k - 1]) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if (in_len && e[PSZHEADER_ENC_PASS2_END] > in_len) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if ((size_t)e[PSZHEADER_ENC_PASS1_END] - e[PSZHEADER_SPFMT] != 8 * m->header->splen) return PSZ_ABORT_NOT_IMPLEMENTED;
   if ((sizeof(T) == 4) != (m->header->dtype == F4)) return PSZ_ABORT_UNSUPPORTED_TYPE;
   CUSZ_AMD_HIP_CHECK(hipSetDevice(p->device));
   int s = p->decompress<T>(m->header, in, out);

@@ -355,12 +355,9 @@ __global__ void __launch_bounds__(kSplThreads) k_spline3_x(SplineXArgs<T> a)
 
 int spl_grid(const void* fn, size_t lds, uint32_t ntiles)
 {
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
-  }
+  int dev = 0, ncu = 0;  // the current device (no process-global cache: several GPUs per process)
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kSplThreads, lds) != hipSuccess || per_cu < 1)
     per_cu = 1;
