@@ -149,8 +149,10 @@ struct SplineXArgs {
   uint32_t gdx, gdy, gdz, ntiles;
   float eb_r, ebx2;
   int radius;
-  const uint32_t* boff = nullptr;   // per-tile bucket offsets (set by the launcher)
-  const uint64_t* bucket = nullptr; // outlier cells grouped by tile
+  const uint32_t* boff = nullptr;     // per-tile bucket offsets (set by the launcher)
+  const uint32_t* bucket = nullptr;   // outlier cells {code bits, idx} grouped by tile (unsorted archives)
+  const uint32_t* cells = nullptr;    // the archive's cells (already grouped: archives of this compressor)
+  const uint32_t* unsorted = nullptr; // device flag: use `bucket` instead of `cells`
   size_t nbucket = 0;
 };
 // cells: the archive's outlier segment ({f32 code, u32 idx} each); scratch: spline_x_scratch_words

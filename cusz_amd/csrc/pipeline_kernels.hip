@@ -139,7 +139,23 @@ __global__ void __launch_bounds__(256) k_extrema_partial(const T* __restrict__ i
 {
   __shared__ T s_mn[4], s_mx[4];
   T mn = INFINITY, mx = -INFINITY;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+  // 16-B loads, two in flight per lane per iteration; the scalar tail covers n % per-iteration
+  constexpr int E = 16 / sizeof(T);
+  const bool aligned = ((uintptr_t)in & 15) == 0;  // a caller may pass any element-aligned pointer
+  const size_t nv = aligned ? n / (2 * E) : 0, stride = (size_t)gridDim.x * blockDim.x;
+  const uint4* in4 = reinterpret_cast<const uint4*>(in);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nv; i += stride) {
+    const uint4 a = in4[2 * i], b = in4[2 * i + 1];
+    T v[2 * E];
+    __builtin_memcpy(&v[0], &a, 16);
+    __builtin_memcpy(&v[E], &b, 16);
+#pragma unroll
+    for (int k = 0; k < 2 * E; k++) {
+      mn = v[k] < mn ? v[k] : mn;
+      mx = v[k] > mx ? v[k] : mx;
+    }
+  }
+  for (size_t i = nv * 2 * E + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += stride) {
     const T v = in[i];
     mn = v < mn ? v : mn;
     mx = v > mx ? v : mx;
@@ -160,12 +176,30 @@ __global__ void __launch_bounds__(256) k_extrema_partial(const T* __restrict__ i
   }
 }
 
-__global__ void k_extrema_final(const double* part, int nparts, double* out)
+// one 256-thread block reduces the per-block partials (extrema.cuhip.inl:150-208 does the same
+// final step with a second kernel launch)
+__global__ void __launch_bounds__(256) k_extrema_final(const double* part, int nparts, double* out)
 {
-  if (threadIdx.x != 0) return;
+  __shared__ double s_mn[4], s_mx[4];
   double mn = INFINITY, mx = -INFINITY;
-  for (int i = 0; i < nparts; i++) mn = part[2 * i] < mn ? part[2 * i] : mn, mx = part[2 * i + 1] > mx ? part[2 * i + 1] : mx;
-  out[0] = mn, out[1] = mx;
+  for (int i = threadIdx.x; i < nparts; i += 256) {
+    const double a = part[2 * i], b = part[2 * i + 1];
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    const double a = __shfl_xor(mn, d), b = __shfl_xor(mx, d);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) s_mn[wid] = mn, s_mx[wid] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; w++) mn = s_mn[w] < mn ? s_mn[w] : mn, mx = s_mx[w] > mx ? s_mx[w] : mx;
+    out[0] = mn, out[1] = mx;
+  }
 }
 
 // Copy device words into host-mapped (coherent, pinned) memory, then raise a flag the host
@@ -236,7 +270,7 @@ int launch_extrema(const T* in, size_t n, double* d_minmax, unsigned int* d_scra
   if (grid > 1024) grid = 1024;
   if (grid < 1) grid = 1;
   k_extrema_partial<T><<<grid, 256, 0, st>>>(in, n, part);
-  k_extrema_final<<<1, 64, 0, st>>>(part, grid, d_minmax);
+  k_extrema_final<<<1, 256, 0, st>>>(part, grid, d_minmax);
   return (int)hipGetLastError();
 }
 

@@ -247,10 +247,38 @@ __device__ __forceinline__ uint32_t tile_of_index(uint32_t gid, uint32_t X, uint
   return gx / 32 + gdx * (gy / 8 + gdy * (gz / 8));
 }
 
+// Archives written by this compressor list outlier cells tile by tile (ranged spill, see
+// OutlierSink::spill_start), so the cells already ARE the buckets: one pass finds each tile's
+// first cell (no atomics).  Any descent in tile order sets *unsorted and the count / scan / fill
+// kernels below build the buckets instead (they return at once when the cells are sorted).
+__global__ void __launch_bounds__(256) k_spl_bucket_bounds(const uint32_t* cells, size_t ncell, size_t n, uint32_t X,
+                                                           uint32_t Y, uint32_t gdx, uint32_t gdy, uint32_t ntiles,
+                                                           uint32_t* off, uint32_t* unsorted)
+{
+  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < ncell; i += (size_t)gridDim.x * 256) {
+    const uint32_t gid = cells[2 * i + 1];
+    if (gid >= n) {
+      atomicOr(unsorted, 1u);
+      continue;
+    }
+    const int64_t t = tile_of_index(gid, X, Y, gdx, gdy);
+    int64_t tp = -1;
+    if (i > 0) {
+      const uint32_t gp = cells[2 * i - 1];
+      tp = gp < n ? (int64_t)tile_of_index(gp, X, Y, gdx, gdy) : (int64_t)ntiles;
+    }
+    if (t < tp) atomicOr(unsorted, 1u);
+    for (int64_t u = tp + 1; u <= t; u++) off[u] = (uint32_t)i;
+    if (i + 1 == ncell)
+      for (int64_t u = t + 1; u <= (int64_t)ntiles; u++) off[u] = (uint32_t)ncell;
+  }
+}
+
 __global__ void __launch_bounds__(256) k_spl_bucket_count(const uint32_t* cells, size_t ncell, size_t n,
                                                           uint32_t X, uint32_t Y, uint32_t gdx, uint32_t gdy,
-                                                          uint32_t* cnt)
+                                                          uint32_t* cnt, const uint32_t* unsorted)
 {
+  if (!*unsorted) return;
   for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < ncell; i += (size_t)gridDim.x * 256) {
     const uint32_t gid = cells[2 * i + 1];
     if (gid < n) atomicAdd(&cnt[tile_of_index(gid, X, Y, gdx, gdy)], 1u);
@@ -258,8 +286,10 @@ __global__ void __launch_bounds__(256) k_spl_bucket_count(const uint32_t* cells,
 }
 
 // exclusive scan of cnt[0..m) into off[0..m], one workgroup of 1024 threads, sequential chunks
-__global__ void __launch_bounds__(1024) k_spl_bucket_scan(const uint32_t* cnt, uint32_t m, uint32_t* off)
+__global__ void __launch_bounds__(1024) k_spl_bucket_scan(const uint32_t* cnt, uint32_t m, uint32_t* off,
+                                                          const uint32_t* unsorted)
 {
+  if (!*unsorted) return;
   __shared__ uint32_t s_w[16];
   __shared__ uint32_t s_carry;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -288,14 +318,16 @@ __global__ void __launch_bounds__(1024) k_spl_bucket_scan(const uint32_t* cnt, u
 
 __global__ void __launch_bounds__(256) k_spl_bucket_fill(const uint32_t* cells, size_t ncell, size_t n, uint32_t X,
                                                          uint32_t Y, uint32_t gdx, uint32_t gdy, const uint32_t* off,
-                                                         uint32_t* fill, uint64_t* bucket)
+                                                         uint32_t* fill, uint32_t* bucket, const uint32_t* unsorted)
 {
+  if (!*unsorted) return;
   for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < ncell; i += (size_t)gridDim.x * 256) {
     const uint32_t v = cells[2 * i], gid = cells[2 * i + 1];
     if (gid >= n) continue;
     const uint32_t tl = tile_of_index(gid, X, Y, gdx, gdy);
     const uint32_t p = off[tl] + atomicAdd(&fill[tl], 1u);
-    bucket[p] = (uint64_t)v | ((uint64_t)gid << 32);
+    bucket[2 * p] = v;
+    bucket[2 * p + 1] = gid;
   }
 }
 
@@ -332,13 +364,13 @@ __global__ void __launch_bounds__(kSplThreads) k_spline3_x(SplineXArgs<T> a)
         if (nbx >= a.gdx || nby >= a.gdy || nbz >= a.gdz) continue;
         const uint32_t nt = nbx + a.gdx * (nby + a.gdy * nbz);
         const uint32_t b0 = a.boff[nt], b1 = a.boff[nt + 1];
+        const uint32_t* bk = *a.unsorted ? a.bucket : a.cells;
         for (uint32_t j = b0 + tid; j < b1; j += kSplThreads) {
-          const uint64_t c = a.bucket[j];
-          const uint32_t gid = (uint32_t)(c >> 32);
+          const uint32_t cv = bk[2 * j], gid = bk[2 * j + 1];
           const uint32_t gx = gid % X, gy = (gid / X) % Y, gz = gid / (X * Y);
           const int lx = (int)gx - (int)(t.bx * 32), ly = (int)gy - (int)(t.by * 8), lz = (int)gz - (int)(t.bz * 8);
           if (lx >= 0 && lx < kSX && ly >= 0 && ly < kSY && lz >= 0 && lz < kSZ)
-            s_code[sidx(lx, ly, lz)] = (int)__builtin_bit_cast(float, (uint32_t)c);
+            s_code[sidx(lx, ly, lz)] = (int)__builtin_bit_cast(float, cv);
         }
       }
       __syncthreads();
@@ -389,28 +421,32 @@ template <typename T>
 int launch_spline3_x(SplineXArgs<T> a, const uint32_t* cells, size_t ncell, uint32_t* scratch, hipStream_t st)
 {
   if (a.ntiles == 0) return 0;
-  // scratch: cnt[ntiles] | fill[ntiles] | off[ntiles+1] | (8-B aligned) bucket[ncell]
+  // scratch: cnt[ntiles] | fill[ntiles] | off[ntiles+1] | unsorted | bucket[2 ncell]
   a.nbucket = ncell;
   if (ncell) {
     uint32_t* cnt = scratch;
     uint32_t* fill = scratch + a.ntiles;
     uint32_t* off = scratch + 2 * (size_t)a.ntiles;
-    uint64_t* bucket = reinterpret_cast<uint64_t*>(scratch + ((3 * (size_t)a.ntiles + 2 + 1) & ~(size_t)1));
+    uint32_t* unsorted = off + a.ntiles + 1;
+    uint32_t* bucket = unsorted + 1;
     const size_t n = (size_t)a.X * a.Y * a.Z;
-    if (hipMemsetAsync(scratch, 0, 2 * (size_t)a.ntiles * 4, st) != hipSuccess) return (int)hipGetLastError();
+    if (hipMemsetAsync(scratch, 0, (3 * (size_t)a.ntiles + 2) * 4, st) != hipSuccess) return (int)hipGetLastError();
     const int gb = (int)std::min<size_t>((ncell + 255) / 256, 4096);
-    k_spl_bucket_count<<<gb, 256, 0, st>>>(cells, ncell, n, a.X, a.Y, a.gdx, a.gdy, cnt);
-    k_spl_bucket_scan<<<1, 1024, 0, st>>>(cnt, a.ntiles, off);
-    k_spl_bucket_fill<<<gb, 256, 0, st>>>(cells, ncell, n, a.X, a.Y, a.gdx, a.gdy, off, fill, bucket);
+    k_spl_bucket_bounds<<<gb, 256, 0, st>>>(cells, ncell, n, a.X, a.Y, a.gdx, a.gdy, a.ntiles, off, unsorted);
+    k_spl_bucket_count<<<gb, 256, 0, st>>>(cells, ncell, n, a.X, a.Y, a.gdx, a.gdy, cnt, unsorted);
+    k_spl_bucket_scan<<<1, 1024, 0, st>>>(cnt, a.ntiles, off, unsorted);
+    k_spl_bucket_fill<<<gb, 256, 0, st>>>(cells, ncell, n, a.X, a.Y, a.gdx, a.gdy, off, fill, bucket, unsorted);
     a.boff = off;
     a.bucket = bucket;
+    a.cells = cells;
+    a.unsorted = unsorted;
   }
   const int grid = spl_grid((const void*)k_spline3_x<T>, 0, a.ntiles);
   k_spline3_x<T><<<grid, kSplThreads, 0, st>>>(a);
   return (int)hipGetLastError();
 }
 
-size_t spline_x_scratch_words(uint32_t ntiles, size_t ncell) { return 3 * (size_t)ntiles + 4 + 2 * ncell; }
+size_t spline_x_scratch_words(uint32_t ntiles, size_t ncell) { return 3 * (size_t)ntiles + 4 + 2 * ncell; }  // + unsorted flag fits the +4
 
 template int launch_spline3_c<float>(const SplineArgs<float>&, hipStream_t);
 template int launch_spline3_c<double>(const SplineArgs<double>&, hipStream_t);
