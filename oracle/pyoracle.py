@@ -80,6 +80,9 @@ def ref():
         R.ref_c_lorenzo_f32.restype = C.c_uint32
         R.ref_c_lorenzo_f32.argtypes = [_P, _SZ, _SZ, _SZ, C.c_double, C.c_uint16, _P, _P, _P, _SZ]
         R.ref_x_lorenzo_f32.argtypes = [_P, _P, _P, _SZ, _SZ, _SZ, C.c_double, C.c_uint16]
+        for fn in (R.ref_c_lorenzo_zz_f32, R.ref_c_lorenzo3d_f64):
+            fn.restype = C.c_uint32
+            fn.argtypes = [_P, _SZ, _SZ, _SZ, C.c_double, C.c_uint16, _P, _P, _P, _SZ]
         R.ref_scatter_f32.argtypes = [_P, _P, C.c_uint32, _P]
         R.ref_histogram_u2.argtypes = [_P, _SZ, _P, C.c_uint16]
         R.ref_build_codebook_u2.restype = C.c_int
@@ -256,6 +259,30 @@ def ref_lorenzo_c_f32(data, dims, eb, radius=512):
     ov = np.zeros(n + 1, np.float32)
     oi = np.zeros(n + 1, np.uint32)
     k = ref().ref_c_lorenzo_f32(_ptr(data), x, y, z, eb, radius, _ptr(codes), _ptr(ov), _ptr(oi), n)
+    return codes, ov[:k].copy(), oi[:k].copy()
+
+
+def ref_lorenzo_c_zz_f32(data, dims, eb, radius=512):
+    """Reference CPU ZigZag Lorenzo (CPU_c_lorenzo_nd_with_outlier<f4,true,u2>, lrz.seq.cc:82)."""
+    data = np.ascontiguousarray(data, np.float32)
+    x, y, z = dims
+    n = x * y * z
+    codes = np.zeros(n, np.uint16)
+    ov = np.zeros(n + 1, np.float32)
+    oi = np.zeros(n + 1, np.uint32)
+    k = ref().ref_c_lorenzo_zz_f32(_ptr(data), x, y, z, eb, radius, _ptr(codes), _ptr(ov), _ptr(oi), n)
+    return codes, ov[:k].copy(), oi[:k].copy()
+
+
+def ref_lorenzo3d_f64(data, dims, eb, radius=512):
+    """Reference CPU 3-D Lorenzo template (KERNEL_SEQ_c_lorenzo_3d1l, lrz.seq.inl) for double."""
+    data = np.ascontiguousarray(data, np.float64)
+    x, y, z = dims
+    n = x * y * z
+    codes = np.zeros(n, np.uint16)
+    ov = np.zeros(n + 1, np.float32)
+    oi = np.zeros(n + 1, np.uint32)
+    k = ref().ref_c_lorenzo3d_f64(_ptr(data), x, y, z, eb, radius, _ptr(codes), _ptr(ov), _ptr(oi), n)
     return codes, ov[:k].copy(), oi[:k].copy()
 
 

@@ -10,6 +10,8 @@
 // Wrapped reference entry points:
 //   psz::module::CPU_c_lorenzo_nd_with_outlier<f4,false,u2>::kernel   psz/src/kernel/lrz.seq.cc:35-55
 //   psz::module::CPU_x_lorenzo_nd<f4,false,u2>::kernel                psz/src/kernel/lrz.seq.cc:57-77
+//   psz::module::CPU_c_lorenzo_nd_with_outlier<f4,true,u2>::kernel    psz/src/kernel/lrz.seq.cc:82 (ZigZag)
+//   psz::KERNEL_SEQ_c_lorenzo_3d1l<f8,false,u2>                       psz/src/kernel/detail/lrz.seq.inl:351-406
 //   psz::KERNEL_SEQ_{c,x}_lorenzo_{1,2,3}d1l                          psz/src/kernel/detail/lrz.seq.inl:154-545
 //   psz::module::SEQ_histogram_generic<u2>                            psz/src/kernel/hist_generic.seq.cc:17-30
 //   phf_CPU_build_canonized_codebook_v2<u2,u4>                        codec/hf/src/hf_bk.seq.cc:72-145
@@ -19,6 +21,12 @@
 #include <cstdint>
 #include <cstring>
 #include <memory>
+
+// the 3-D template, instantiated below for f8; its file-scope helper object `div3` is renamed
+// here so that it does not collide with lrz.seq.cc's copy at link time
+#define div3 ref_shim_div3
+#include "kernel/detail/lrz.seq.inl"
+#undef div3
 
 #include "c_type.h"
 #include "hf_impl.hh"
@@ -48,6 +56,42 @@ uint32_t ref_c_lorenzo_f32(
   uint32_t n = outlier->num();
   for (uint32_t i = 0; i < n; i++) {
     ol_val[i] = outlier->val_idx(i).val;
+    ol_idx[i] = outlier->val_idx(i).idx;
+  }
+  return n;
+}
+
+// ZigZag variant (the reference's own instantiation, lrz.seq.cc:82).
+uint32_t ref_c_lorenzo_zz_f32(
+    const float* in, size_t x, size_t y, size_t z, double eb, uint16_t radius, uint16_t* codes,
+    float* ol_val, uint32_t* ol_idx, size_t ol_cap)
+{
+  auto outlier = std::make_unique<_portable::compact_CPU<f4, u4>>(ol_cap);
+  psz_len len{x, y, z};
+  psz::module::CPU_c_lorenzo_nd_with_outlier<f4, true, u2>::kernel(
+      const_cast<float*>(in), len, codes, outlier.get(), eb, radius, nullptr);
+  uint32_t n = outlier->num();
+  for (uint32_t i = 0; i < n; i++) {
+    ol_val[i] = outlier->val_idx(i).val;
+    ol_idx[i] = outlier->val_idx(i).idx;
+  }
+  return n;
+}
+
+// 3-D f64: the reference's template instantiated for double, called the way
+// CPU_c_lorenzo_nd_with_outlier calls it (lrz.seq.cc:35-55).
+uint32_t ref_c_lorenzo3d_f64(
+    const double* in, size_t x, size_t y, size_t z, double eb, uint16_t radius, uint16_t* codes,
+    float* ol_val, uint32_t* ol_idx, size_t ol_cap)
+{
+  auto outlier = std::make_unique<_portable::compact_CPU<f8>>(ol_cap);
+  psz_len len{x, y, z};
+  auto leap3 = psz_len{1, x, x * y};
+  psz::KERNEL_SEQ_c_lorenzo_3d1l<f8, false, u2>(
+      const_cast<double*>(in), len, leap3, radius, 1 / (eb * 2), codes, outlier.get());
+  uint32_t n = outlier->num();
+  for (uint32_t i = 0; i < n; i++) {
+    ol_val[i] = (float)outlier->val_idx(i).val;
     ol_idx[i] = outlier->val_idx(i).idx;
   }
   return n;

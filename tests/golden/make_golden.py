@@ -106,6 +106,18 @@ def main():
     codes = rng.integers(0, 1024, 100000).astype(np.uint16)
     np.savez_compressed(os.path.join(HERE, "ref_hist.npz"), codes=codes,
                         hist=pyoracle.ref_histogram(codes))
+    # (round 2; own generator so the fixtures above stay as they were)
+    rng2 = np.random.default_rng(20261016)
+    # ZigZag (the reference's own f4 instantiation, lrz.seq.cc:82) and f64 (the 3-D template
+    # instantiated for double by oracle/ref_shim.cc) on the same kind of integer field
+    codes, ov, oi = pyoracle.ref_lorenzo_c_zz_f32(walk, dims, 0.5)
+    np.savez_compressed(os.path.join(HERE, "ref_lrz3d_zz.npz"), data=walk, dims=np.array(dims),
+                        codes=codes, ol_val=ov, ol_idx=oi)
+    walk64 = np.cumsum(rng2.integers(-3, 4, n)).astype(np.float64)
+    walk64[rng2.integers(0, n, 40)] += rng2.integers(-5000, 5000, 40)
+    codes, ov, oi = pyoracle.ref_lorenzo3d_f64(walk64, dims, 0.5)
+    np.savez_compressed(os.path.join(HERE, "ref_lrz3d_f64.npz"), data=walk64, dims=np.array(dims),
+                        codes=codes, ol_val=ov, ol_idx=oi)
     print("fixtures written to", HERE)
 
 

@@ -1,0 +1,67 @@
+"""The GPU path against fixtures produced by the compiled reference itself (tests/golden,
+make_golden.py): Lorenzo-3D f32, its ZigZag instantiation (lrz.seq.cc:82) and the 3-D template
+for double, integer data at eb = 0.5 (where the reference CPU path and the GPU semantics
+coincide).  Also the HACC-like outlier stress of SURVEY §8d config 3."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import cusz_amd as cz
+from cusz_amd import datagen
+from gpu_util import d2h, parse_archive, sync, to_device
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.mark.parametrize("fixture,zigzag", [("ref_lrz3d.npz", False), ("ref_lrz3d_zz.npz", True),
+                                            ("ref_lrz3d_f64.npz", False)])
+def test_gpu_matches_reference_fixture(fixture, zigzag):
+    g = np.load(os.path.join(GOLDEN, fixture))
+    dims = tuple(int(v) for v in g["dims"])
+    data = g["data"]
+    f64 = data.dtype == np.float64
+    r = cz.Resource(cz.F8 if f64 else cz.F4, dims, cz.LorenzoZigZag if zigzag else cz.Lorenzo)
+    d = to_device(data)
+    ptr, nb, _ = r.compress(d.data_ptr(), 0.5)
+    arch = d2h(ptr, nb).tobytes()
+    r.decode_codes(ptr)
+    sync()
+    codes = d2h(r.internals().d_quant_codes, 2 * data.size, np.uint16)
+    np.testing.assert_array_equal(codes, g["codes"])
+    a = parse_archive(arch)
+    order = np.argsort(a["ol_idx"], kind="stable")
+    ref_order = np.argsort(g["ol_idx"], kind="stable")
+    np.testing.assert_array_equal(a["ol_idx"][order], g["ol_idx"][ref_order])
+    np.testing.assert_array_equal(a["ol_val"][order], g["ol_val"][ref_order])
+    out = torch.full((data.size,), float("nan"), dtype=torch.float64 if f64 else torch.float32, device="cuda")
+    r.decompress(ptr, nb, out.data_ptr())
+    sync()
+    np.testing.assert_array_equal(out.cpu().numpy(), data)
+
+
+def test_hacc_jump_stress_overflow_is_reported():
+    """30 % uniform jumps: more outliers than the reference's 10 % cap.  The reference silently
+    drops cells; here compress reports PSZ_WARN_OUTLIER_TOO_MANY."""
+    n = 4_000_000
+    d = datagen.hacc1d_torch(n, seed=7, jump=0.30)
+    r = cz.Resource(cz.F4, (n, 1, 1))
+    with pytest.raises(cz.PszError) as e:
+        r.compress(d.data_ptr(), 1e-4)
+    assert e.value.status == cz.PSZ_WARN_OUTLIER_TOO_MANY
+
+
+def test_hacc_jump_within_cap_roundtrip():
+    n = 4_000_011  # n mod 1024 != 0: partial last tile
+    d = datagen.hacc1d_torch(n, seed=8, jump=0.05)
+    r = cz.Resource(cz.F4, (n, 1, 1))
+    ptr, nb, st = r.compress(d.data_ptr(), 1e-4)
+    assert st == cz.PSZ_SUCCESS
+    assert r.header.splen > 0.04 * n
+    out = torch.empty(n, device="cuda")
+    r.decompress(ptr, nb, out.data_ptr())
+    sync()
+    err = (out.double() - d.double()).abs().max().item()
+    assert err <= 1.001e-4 + 2.0 ** -23 * 256

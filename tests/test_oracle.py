@@ -56,6 +56,21 @@ def test_ref_lorenzo3d_integer_crosscheck(oracle):
     np.testing.assert_array_equal(out, g["data"])
 
 
+@pytest.mark.parametrize("fixture,zigzag", [("ref_lrz3d_zz.npz", True), ("ref_lrz3d_f64.npz", False)])
+def test_ref_lorenzo3d_zigzag_f64_crosscheck(oracle, fixture, zigzag):
+    """Compiled reference on integer data at eb=0.5: the ZigZag instantiation (lrz.seq.cc:82) and
+    the 3-D template for double (lrz.seq.inl, instantiated by oracle/ref_shim.cc)."""
+    g = np.load(os.path.join(GOLDEN, fixture))
+    dims = tuple(int(v) for v in g["dims"])
+    codes, ov, oi = oracle.lorenzo_c(g["data"], dims, eb=0.5, zigzag=zigzag)
+    np.testing.assert_array_equal(codes, g["codes"])
+    order = np.argsort(g["ol_idx"], kind="stable")
+    np.testing.assert_array_equal(oi, g["ol_idx"][order])
+    np.testing.assert_array_equal(ov, g["ol_val"][order])
+    out = oracle.lorenzo_x(codes, ov, oi, dims, eb=0.5, zigzag=zigzag, dtype=g["data"].dtype)
+    np.testing.assert_array_equal(out, g["data"])
+
+
 def test_ref_histogram(oracle):
     g = np.load(os.path.join(GOLDEN, "ref_hist.npz"))
     np.testing.assert_array_equal(oracle.histogram(g["codes"]), g["hist"])
