@@ -118,6 +118,8 @@ struct Pipeline {
   // pinned, host-mapped, coherent transfer area (kernels write it, the host polls flags)
   uint8_t* h_xfer = nullptr;
   uint32_t epoch = 0;
+  uint32_t gate_epoch = 0;       // host -> stream gate (flag 5): the stream waits on it
+  bool can_wait_value = false;   // hipStreamWaitValue32 on host-mapped memory
   static constexpr size_t kXferBytes = 16384;
   volatile uint32_t* flag(int i) { return reinterpret_cast<volatile uint32_t*>(h_xfer) + i; }  // 0..15
   uint32_t* h_hist() { return reinterpret_cast<uint32_t*>(h_xfer + 64); }               // 4 KB
@@ -225,6 +227,9 @@ struct Pipeline {
     CUSZ_AMD_HIP_CHECK(hipHostMalloc(&h_xfer, kXferBytes, hipHostMallocMapped | hipHostMallocCoherent));
     std::memset(h_xfer, 0, kXferBytes);
     for (auto& e : ev) CUSZ_AMD_HIP_CHECK(hipEventCreate(&e));
+    int wv = 0;
+    if (hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, device) == hipSuccess) can_wait_value = wv;
+    if (const char* g = getenv("CUSZ_AMD_NO_GATE")) can_wait_value = can_wait_value && atoi(g) == 0;
     return PSZ_SUCCESS;
   }
 
@@ -251,6 +256,11 @@ struct Pipeline {
   {
     const uint32_t e = ++epoch;
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_publish(r, const_cast<uint32_t*>(flag(fl)), e, stream));
+    return wait_flag(fl, e);
+  }
+
+  int wait_flag(int fl, uint32_t e)
+  {
     for (long spin = 0;; spin++) {
       if (__atomic_load_n(flag(fl), __ATOMIC_ACQUIRE) == e) return PSZ_SUCCESS;
       if (spin > (1L << 26)) break;  // ~seconds: something is wrong, surface it via the runtime
@@ -471,11 +481,26 @@ struct Pipeline {
     const BrickGeom& g = bl.g;
     const int bsub = g.W, bpar = (int)g.nchunks;
     const uint32_t cap = brick_cap();
-    int fs = fetch(regions({{h_hist(), d_hist, (size_t)bklen * 4}}), 2);
-    if (fs) return fs;
-    const int rv = build_codebook(h_hist(), bklen, h_book(), h_revbook());
+    // The histogram goes to the host; the codebook comes back through host-mapped memory.  When
+    // the device supports stream waits, every launch after the codebook is queued NOW behind a
+    // gate the host opens once the book is built: the kernels start the moment it is ready
+    // instead of after their launch latency.
+    const uint32_t eh = ++epoch;
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_publish(regions({{h_hist(), d_hist, (size_t)bklen * 4}}),
+                                                  const_cast<uint32_t*>(flag(2)), eh, stream));
+    const uint32_t eg = ++gate_epoch;
+    const bool gated =
+        can_wait_value && hipStreamWaitValue32(stream, (void*)flag(5), eg, hipStreamWaitValueGte) == hipSuccess;
+    auto build_book = [&]() -> int {
+      int fs = wait_flag(2, eh);
+      if (!fs) build_codebook(h_hist(), bklen, h_book(), h_revbook());
+      if (gated) __atomic_store_n(flag(5), eg, __ATOMIC_RELEASE);  // always open the gate
+      return fs;
+    };
+    if (!gated)
+      if (int fs = build_book()) return fs;
     const size_t phf_off = 176;
-    const size_t rvbk = (size_t)rv;
+    const size_t rvbk = rvbk_bytes(bklen);
     const size_t nbit_rel = 128 + rvbk, entry_rel = nbit_rel + 4 * (size_t)bpar;
     const size_t bits_rel = entry_rel + 4 * (size_t)bpar;
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_upload(
@@ -505,6 +530,8 @@ struct Pipeline {
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_pack(bl, d_codes, d_book, bklen, pa, par_nbit, par_entry, bits,
                                                      pack_reverse, timeout(), stream));
     mark(4);
+    if (gated)
+      if (int fs = build_book()) return fs;
     mark(5);
     return finish_compress(h, out, outlen);
   }
