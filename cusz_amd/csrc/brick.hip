@@ -119,6 +119,25 @@ struct StepLoader {
   // Rows (y, z = 0..7) of brick `it` by raw buffer loads from the brick's origin: one 16-B (f64:
   // two) load per lane and row, rows outside the field get an offset past the range and read 0.
   // Straight-line code: no per-row branches, so the waitcnt pass can count the loads exactly.
+  // row `row` = 8 y + z of brick `it` (rows outside the field read 0)
+  __device__ __forceinline__ void issue_row(uint32_t it, int row, T (&dst)[V]) const
+  {
+    if (it >= nbricks) return;
+    const uint32_t b = brick_of(it), bx = b % nbx, t = b / nbx, by = t % nby, bz = t / nby;
+    const T* origin = in + (size_t)bz * 8 * plane + (size_t)by * 8 * lx + (size_t)bx * (64 * V);
+    const uint32_t span = (uint32_t)(8 * plane * sizeof(T));  // < 2^31 (brick_geom)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(origin), 0, (int)span, 0x00020000);
+    const uint32_t y = (uint32_t)row >> 3, z = (uint32_t)row & 7u;
+    const bool ok = by * 8 + y < ly && bz * 8 + z < lz;
+    const uint32_t off =
+        ok ? (uint32_t)(((size_t)z * plane + (size_t)y * lx) * sizeof(T)) + lane * (V * sizeof(T)) : span;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int h = 0; h < (int)(V * sizeof(T) / 16); h++) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + 16 * h), 0, 0);
+      __builtin_memcpy(reinterpret_cast<char*>(&dst[0]) + 16 * h, &v, 16);
+    }
+  }
   __device__ __forceinline__ void issue(uint32_t it, int y, T (&dst)[8][V]) const
   {
     if (it >= nbricks) return;
@@ -156,6 +175,18 @@ __device__ __forceinline__ void store_codes_row(uint16_t* p, const uint16_t (&q)
 // =========================================================================================
 // pass 1: predict -> histograms + outliers
 // =========================================================================================
+// Rows are streamed: one brick row (y, z) at a time, in (y, z) order, with the z-diff against
+// the previous row of the same y-step and the y-diff against row (y - 1, z) kept in registers
+// (bprev).  kScanAhead rows (two y-steps) are in flight per wave, loaded into a register queue
+// whose slot is the row's position modulo kScanAhead (the row loop is unrolled by kScanAhead, so
+// the queue needs no copies); the loads run across brick boundaries.  About 110 VGPRs: four
+// waves per SIMD.
+template <typename T>
+#ifndef CUSZ_AMD_SCAN_AHEAD
+#define CUSZ_AMD_SCAN_AHEAD 16
+#endif
+constexpr int kScanAhead = sizeof(T) == 4 ? CUSZ_AMD_SCAN_AHEAD : 8;
+
 template <typename T, int V, bool ZZ>
 __global__ void __launch_bounds__(64 * kBrickWaves)
 k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T ebx2_r, T r, OutlierSink ol,
@@ -175,11 +206,12 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
   const size_t plane = ld.plane;
   const uint32_t nunits = (nbricks + kUnitBricks - 1) / kUnitBricks;
   const int hs = bhist_stride(bklen);
+  constexpr int D = kScanAhead<T>;
+  static_assert(64 % D == 0 && D % 8 == 0, "the queue holds whole y-steps");
   uint32_t u = blockIdx.x * kBrickWaves + wid;
-  constexpr int NB = kStepBuffers<T>;
-  T buf[NB][8][V];
+  T q[D][V];
 #pragma unroll
-  for (int j = 0; j < NB; j++) ld.issue(u * kUnitBricks, j, buf[j]);
+  for (int j = 0; j < D; j++) ld.issue_row(u * kUnitBricks, j, q[j]);
   for (; u < nunits; u += nw) {
     uint32_t cnt = 0;
     const uint32_t bend = min((u + 1) * kUnitBricks, nbricks);
@@ -187,45 +219,67 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
       const uint32_t bnext = brick + 1 < bend ? brick + 1 : (u + nw) * kUnitBricks;  // next brick of the stream
       const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
       const uint32_t x0 = bx * (64 * V) + lane * V, y0 = by * 8, z0 = bz * 8;
-      T bprev[8][V];
+      uint16_t* cbrick = bcodes + (size_t)brick * 64 * (64 * V) + (size_t)lane * V;
+      T bprev[8][V], pprev[V];
 #pragma unroll 1
-      for (int y2 = 0; y2 < 8; y2 += NB)  // not unrolled: instruction cache
+      for (int r0 = 0; r0 < 64; r0 += D)  // not unrolled: instruction cache
 #pragma unroll
-        for (int j = 0; j < NB; j++) {
-          const int y = y2 + j;
-          T d[8][V];
-          prequant_ystep<T, V>(buf[j], ebx2_r, d);
-          if (y + NB < 8) ld.issue(brick, y + NB, buf[j]);
-          else ld.issue(bnext, y + NB - 8, buf[j]);
-          const uint32_t gy = y0 + y;
-          if (gy >= ly) continue;
-          residual_ystep<T, V>(x0, y, bprev, d);
-          uint16_t* crow = bcodes + ((size_t)brick * 64 + (size_t)y * 8) * (64 * V) + (size_t)lane * V;
+        for (int j = 0; j < D; j++) {
+          const int row = r0 + j, z = j & 7, y = row >> 3;
+          T p[V];
 #pragma unroll
-          for (int z = 0; z < 8; z++) {
-            if (z0 + z >= lz) break;
-            float olv[V];
-            uint16_t q[V];
-            uint64_t anyol = 0;  // SALU: OR of the per-element outlier lane masks
+          for (int k = 0; k < V; k++) p[k] = dround(q[j][k] * ebx2_r);
+          if (row + D < 64) ld.issue_row(brick, row + D, q[j]);
+          else ld.issue_row(bnext, row + D - 64, q[j]);
+          const uint32_t gy = y0 + (uint32_t)y;
+#ifdef CUSZ_AMD_DIAG_MEMONLY  // diagnostic: the loads and code stores only (memory floor)
+          {
+            uint16_t qc[V];
+#pragma unroll
+            for (int k = 0; k < V; k++) qc[k] = (uint16_t)(uint32_t)p[k];
+            if (gy < ly && z0 + (uint32_t)z < lz) store_codes_row<V>(cbrick + (size_t)row * (64 * V), qc);
+            continue;
+          }
+#endif
+          // z-diff (lrz_c.cuhip.inl:341-352 order: z, then x inside the 8-wide tile, then y)
+          T a[V];
+#pragma unroll
+          for (int k = 0; k < V; k++) {
+            a[k] = z > 0 ? p[k] - pprev[k] : p[k];
+            pprev[k] = p[k];
+          }
+          const T west = shr_in_tile<T, 1, 8 / V>(a[V - 1]);
+#pragma unroll
+          for (int k = V - 1; k > 0; k--) a[k] = a[k] - a[k - 1];
+          if (x0 % 8 != 0) a[0] = a[0] - west;
+          T d[V];
+#pragma unroll
+          for (int k = 0; k < V; k++) {
+            d[k] = y > 0 ? a[k] - bprev[z][k] : a[k];
+            bprev[z][k] = a[k];
+          }
+          if (gy >= ly || z0 + (uint32_t)z >= lz) continue;  // outside the field (wave-uniform)
+          float olv[V];
+          uint16_t qc[V];
+          uint64_t anyol = 0;  // SALU: OR of the per-element outlier lane masks
+#pragma unroll
+          for (int k = 0; k < V; k++) {
+            bool is_ol;
+            qc[k] = quantize<T, ZZ>(d[k], r, is_ol, olv[k]);
+            anyol |= __ballot(is_ol);
+            atomicAdd(&s_hist[qc[k] * kHistCopies + hc], 1u);
+          }
+          store_codes_row<V>(cbrick + (size_t)row * (64 * V), qc);
+          if (anyol) {
+            uint32_t mask = 0;
+            size_t idx[V];
+            const size_t base = (size_t)(z0 + z) * plane + (size_t)gy * lx;
 #pragma unroll
             for (int k = 0; k < V; k++) {
-              bool is_ol;
-              q[k] = quantize<T, ZZ>(d[z][k], r, is_ol, olv[k]);
-              anyol |= __ballot(is_ol);
-              atomicAdd(&s_hist[q[k] * kHistCopies + hc], 1u);
+              mask |= (uint32_t)(qc[k] == 0 && (ZZ ? !(dabs(d[k]) < r) : true)) << k;
+              idx[k] = base + x0 + k;
             }
-            store_codes_row<V>(crow + (size_t)z * (64 * V), q);
-            if (anyol) {
-              uint32_t mask = 0;
-              size_t idx[V];
-              const size_t base = (size_t)(z0 + z) * plane + (size_t)gy * lx;
-#pragma unroll
-              for (int k = 0; k < V; k++) {
-                mask |= (uint32_t)(q[k] == 0 && (ZZ ? !(dabs(d[z][k]) < r) : true)) << k;
-                idx[k] = base + x0 + k;
-              }
-              emit_outliers<V>(ol, u, cnt, mask, olv, idx);  // one slot per unit
-            }
+            emit_outliers<V>(ol, u, cnt, mask, olv, idx);  // one slot per unit
           }
         }
     }
@@ -496,7 +550,7 @@ k_brick3_pack(const uint16_t* __restrict__ bcodes, uint32_t ly, uint32_t lz, con
 // reads HBM.  The decode step keeps only a bit position: peek 32 bits at `pos` from the word
 // pair, look up one or two codes, store them, advance.
 #ifndef CUSZ_AMD_DEC_B  // tuning knobs (overridable at build time for experiments)
-#define CUSZ_AMD_DEC_B 11
+#define CUSZ_AMD_DEC_B 12
 #endif
 #ifndef CUSZ_AMD_DEC_RING
 #define CUSZ_AMD_DEC_RING 16

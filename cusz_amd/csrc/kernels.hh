@@ -116,6 +116,7 @@ struct XferRegions {
 };
 int launch_publish(const XferRegions& r, uint32_t* flag, uint32_t epoch, hipStream_t st);
 int launch_upload(const XferRegions& r, hipStream_t st);
+int launch_zero(const XferRegions& r, hipStream_t st);  // dst/nwords only
 
 // ---- cuSZ-i spline3 (spline.hip) -----------------------------------------------------------
 struct SplineGeom {

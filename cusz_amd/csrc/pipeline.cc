@@ -354,9 +354,14 @@ struct Pipeline {
     const double eb = h->rc.eb;
 
     // per-call state reset (the reference never resets these: SURVEY.md Appendix B.3)
-    CUSZ_AMD_HIP_CHECK(hipMemsetAsync(d_hist, 0, (size_t)bklen * 4, stream));
-    CUSZ_AMD_HIP_CHECK(hipMemsetAsync(d_small, 0, 64 + sizeof(CompressInfo), stream));
-    if (!brick) CUSZ_AMD_HIP_CHECK(hipMemsetAsync(d_status, 0, status_words * 8, stream));
+    if (brick)
+      CUSZ_AMD_HIP_CHECK((hipError_t)launch_zero(
+          regions({{d_hist, nullptr, (size_t)bklen * 4}, {d_small, nullptr, 64 + sizeof(CompressInfo)}}), stream));
+    else
+      CUSZ_AMD_HIP_CHECK((hipError_t)launch_zero(regions({{d_hist, nullptr, (size_t)bklen * 4},
+                                                          {d_small, nullptr, 64 + sizeof(CompressInfo)},
+                                                          {d_status, nullptr, status_words * 8}}),
+                                                 stream));
     mark(1);
     last_layout = brick ? PSZ_AMD_LAYOUT_BRICK : PSZ_AMD_LAYOUT_REFERENCE;
     pend.brick = brick, pend.spl = spl, pend.radius = radius;
@@ -559,7 +564,7 @@ struct Pipeline {
       stage_ms[PSZ_AMD_T_FINALIZE] = span(4, 5);
       stage_ms[PSZ_AMD_T_COMPRESS] = span(0, 5);
     }
-#ifdef CUSZ_AMD_DIAG_NOHIST  // diagnostic build: the reservation is knowingly wrong
+#if defined(CUSZ_AMD_DIAG_NOHIST) || defined(CUSZ_AMD_DIAG_MEMONLY)  // diagnostic builds: wrong reservation
     tmo = 0;
 #endif
     if (tmo) {
@@ -647,7 +652,7 @@ struct Pipeline {
     const size_t bits_off = phf_off + 128 + rvbk + 8 * (size_t)pd;
     const size_t total = h->entry[PSZHEADER_ENC_PASS2_END];
     const size_t bs_words = total > bits_off ? (total - bits_off) / 4 : 0;
-    CUSZ_AMD_HIP_CHECK(hipMemsetAsync(work_counter(), 0, kWorkBytes, stream));
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_zero(regions({{work_counter(), nullptr, kWorkBytes}}), stream));
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_decode<T>(
         bl, reinterpret_cast<const uint32_t*>(phf + 128 + rvbk + 8 * (size_t)pd), bs_words, phf + 128, bklen,
         reinterpret_cast<const uint32_t*>(phf + 128 + rvbk), reinterpret_cast<const uint32_t*>(phf + 128 + rvbk + 4 * (size_t)pd),

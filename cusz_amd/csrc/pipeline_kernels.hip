@@ -213,6 +213,14 @@ __global__ void __launch_bounds__(256) k_publish(XferRegions r, uint32_t* flag, 
   if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Zero up to 4 small device regions in one launch (per-call state reset: cheaper than one
+// hipMemsetAsync per region on the compress critical path).
+__global__ void __launch_bounds__(256) k_zero(XferRegions r)
+{
+  for (int k = 0; k < r.count; k++)
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < r.nwords[k]; i += gridDim.x * 256) r.dst[k][i] = 0u;
+}
+
 // Copy host-mapped words (written by the host before this launch) into device memory.
 __global__ void __launch_bounds__(256) k_upload(XferRegions r)
 {
@@ -225,6 +233,16 @@ __global__ void __launch_bounds__(256) k_upload(XferRegions r)
 int launch_publish(const XferRegions& r, uint32_t* flag, uint32_t epoch, hipStream_t st)
 {
   k_publish<<<1, 256, 0, st>>>(r, flag, epoch);
+  return (int)hipGetLastError();
+}
+
+int launch_zero(const XferRegions& r, hipStream_t st)
+{
+  int words = 0;
+  for (int k = 0; k < r.count; k++) words = r.nwords[k] > words ? r.nwords[k] : words;
+  int grid = (words + 255) / 256;
+  grid = grid < 1 ? 1 : (grid > 256 ? 256 : grid);
+  k_zero<<<grid, 256, 0, st>>>(r);
   return (int)hipGetLastError();
 }
 
