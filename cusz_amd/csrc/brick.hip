@@ -183,7 +183,7 @@ __device__ __forceinline__ void store_codes_row(uint16_t* p, const uint16_t (&q)
 // waves per SIMD.
 template <typename T>
 #ifndef CUSZ_AMD_SCAN_AHEAD
-#define CUSZ_AMD_SCAN_AHEAD 16
+#define CUSZ_AMD_SCAN_AHEAD 8
 #endif
 constexpr int kScanAhead = sizeof(T) == 4 ? CUSZ_AMD_SCAN_AHEAD : 8;
 
@@ -232,15 +232,6 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
           if (row + D < 64) ld.issue_row(brick, row + D, q[j]);
           else ld.issue_row(bnext, row + D - 64, q[j]);
           const uint32_t gy = y0 + (uint32_t)y;
-#ifdef CUSZ_AMD_DIAG_MEMONLY  // diagnostic: the loads and code stores only (memory floor)
-          {
-            uint16_t qc[V];
-#pragma unroll
-            for (int k = 0; k < V; k++) qc[k] = (uint16_t)(uint32_t)p[k];
-            if (gy < ly && z0 + (uint32_t)z < lz) store_codes_row<V>(cbrick + (size_t)row * (64 * V), qc);
-            continue;
-          }
-#endif
           // z-diff (lrz_c.cuhip.inl:341-352 order: z, then x inside the 8-wide tile, then y)
           T a[V];
 #pragma unroll

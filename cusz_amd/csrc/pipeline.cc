@@ -564,7 +564,7 @@ struct Pipeline {
       stage_ms[PSZ_AMD_T_FINALIZE] = span(4, 5);
       stage_ms[PSZ_AMD_T_COMPRESS] = span(0, 5);
     }
-#if defined(CUSZ_AMD_DIAG_NOHIST) || defined(CUSZ_AMD_DIAG_MEMONLY)  // diagnostic builds: wrong reservation
+#ifdef CUSZ_AMD_DIAG_NOHIST  // diagnostic build: the reservation is knowingly wrong
     tmo = 0;
 #endif
     if (tmo) {
