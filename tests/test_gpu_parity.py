@@ -215,3 +215,22 @@ def test_rel_mode(oracle):
     assert h.rc.eb == 1e-4 * rng and h.user_input_eb == 1e-4
     codes_o, _, _ = oracle.lorenzo_c(data, dims, 1e-4 * rng)
     np.testing.assert_array_equal(d2h(r.internals().d_quant_codes, 2 * data.size, np.uint16), codes_o)
+
+
+@pytest.mark.parametrize("decoder", [cz.DECODER_WAVE, cz.DECODER_LANE, cz.DECODER_AUTO])
+def test_long_chunks_high_entropy_all_decoders(oracle, decoder):
+    """sublen 8192 with ~10-bit codes: the wave decoder's LDS staging would exceed its budget,
+    so it stages what fits and reads the rest of a chunk from HBM."""
+    n = 8192 * 6 + 77
+    data = np.random.default_rng(12).random(n).astype(np.float32)
+    r = cz.Resource(cz.F4, (n, 1, 1))
+    r.set_sublen(8192)
+    r.set_decoder(decoder)
+    d_in = to_device(data)
+    ptr, nbytes, _ = r.compress(d_in.data_ptr(), 1e-3)
+    a = parse_archive(d2h(ptr, nbytes).tobytes())
+    assert a["sublen"] == 8192 and a["total_nbit"] > 9 * n
+    r.decode_codes(ptr)
+    sync()
+    codes_o, _, _ = oracle.lorenzo_c(data, (n, 1, 1), 1e-3)
+    np.testing.assert_array_equal(d2h(r.internals().d_quant_codes, 2 * n, np.uint16), codes_o)

@@ -69,8 +69,9 @@ def test_spline_parity(oracle, dims, dtype, eb):
     data, x, ebx, nol = _roundtrip(oracle, dims, dtype, eb)
     err = np.max(np.abs(x.astype(np.float64) - data))
     # the reference quantises with float eb parameters (FP = float, spline3.cu:36) and, for f32,
-    # reconstructs in f32: the bound holds up to those roundings
-    tol = 1.001 if dtype == np.float64 else 1.2
+    # reconstructs in f32: the bound holds up to those roundings.  Measured worst over these
+    # cases (scripts/spline_err.py, round 2): f32 1.00334 eb, f64 1.00031 eb.
+    tol = 1.001 if dtype == np.float64 else 1.005
     assert err <= tol * ebx, (err / ebx, nol)
 
 
