@@ -42,14 +42,20 @@ k_lorenzo_c1d(const T* __restrict__ in, size_t n, T ebx2_r, T r, uint16_t* __res
     uint32_t cnt = 0;
     T carry = 0;
     const size_t bbase = (size_t)brick * 16384;
+    const uint32_t x0 = lane * V;
+    // row s + 1 is loaded while row s is processed (software pipelining of the row loop)
+    T nxt[V];
+    load_row<T, V>(in, bbase, x0, (uint32_t)(n - bbase < 256 ? n - bbase : 256), true, nxt);
     for (int s = 0; s < 64; s++) {
       const size_t base = bbase + (size_t)s * 256;
       // treat [base, n) as one long row of length n - base
       const uint32_t rowlen = (uint32_t)(n - base < 256 ? n - base : 256);
-      const uint32_t x0 = lane * V;
       if (base >= n) break;
       T p[V];
-      load_row<T, V>(in, base, x0, rowlen, true, p);
+#pragma unroll
+      for (int k = 0; k < V; k++) p[k] = nxt[k];
+      const size_t nbase = base + 256;
+      if (s < 63 && nbase < n) load_row<T, V>(in, nbase, x0, (uint32_t)(n - nbase < 256 ? n - nbase : 256), true, nxt);
 #pragma unroll
       for (int k = 0; k < V; k++) p[k] = dround(p[k] * ebx2_r);
       T west = __shfl_up(p[V - 1], 1);
@@ -254,13 +260,42 @@ k_lorenzo_x1d(const uint16_t* __restrict__ codes, T* out, size_t n, T ebx2, T r,
   for (uint32_t brick = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); brick < nbricks; brick += nw) {
     const size_t bbase = (size_t)brick * 16384;
     T carry = 0;
+    const uint32_t x0 = lane * V;
+    // pipelined row loop: codes arrive two rows ahead, the outlier values (read from `out`
+    // where the code is 0) one row ahead, so no row waits on a load it has just issued
+    auto rlen = [&](size_t b0) { return (uint32_t)(n - b0 < 256 ? n - b0 : 256); };
+    uint16_t c1[V], c2[V];
+    T o1[V];
+    load_codes<V>(codes, bbase, x0, rlen(bbase), true, c1);
+    if (bbase + 256 < n) load_codes<V>(codes, bbase + 256, x0, rlen(bbase + 256), true, c2);
+#pragma unroll
+    for (int k = 0; k < V; k++) o1[k] = (x0 + k < rlen(bbase) && c1[k] == 0) ? out[bbase + x0 + k] : T(0);
     for (int s = 0; s < 64; s++) {
       const size_t base = bbase + (size_t)s * 256;
       if (base >= n) break;
-      const uint32_t rowlen = (uint32_t)(n - base < 256 ? n - base : 256);
-      const uint32_t x0 = lane * V;
+      const uint32_t rowlen = rlen(base);
+      uint16_t c[V];
+      T o[V];
+#pragma unroll
+      for (int k = 0; k < V; k++) c[k] = c1[k], o[k] = o1[k];
+      const size_t b1 = base + 256, b2 = base + 512;
+      if (s < 63 && b1 < n) {
+#pragma unroll
+        for (int k = 0; k < V; k++) {
+          c1[k] = c2[k];
+          o1[k] = (x0 + k < rlen(b1) && c1[k] == 0) ? out[b1 + x0 + k] : T(0);
+        }
+        if (s < 62 && b2 < n) load_codes<V>(codes, b2, x0, rlen(b2), true, c2);
+      }
       T b[V];
-      fuse_row<T, V, ZZ>(codes, out, base, x0, rowlen, true, r, b);
+#pragma unroll
+      for (int k = 0; k < V; k++) {
+        const bool in = x0 + k < rowlen;
+        if constexpr (ZZ)
+          b[k] = in ? o[k] + (T)zz_dec(c[k]) : T(0);
+        else
+          b[k] = in ? (o[k] + (T)c[k]) - r : T(0);
+      }
       // per-thread sequential scan (wave32.cuhip.inl:10)
 #pragma unroll
       for (int k = 1; k < V; k++) b[k] = b[k] + b[k - 1];
