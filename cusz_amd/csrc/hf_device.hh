@@ -137,7 +137,10 @@ __device__ __forceinline__ uint32_t tab_decode1(uint32_t v, const uint32_t* firs
 //  Codes longer than 16 bits (or past the cap) count failing lengths against thresholds the
 //  caller keeps in registers (DecRegs).
 constexpr int kL2Bits = 16;
-constexpr int kL2Cap = 4096;
+#ifndef CUSZ_AMD_DEC_L2CAP
+#define CUSZ_AMD_DEC_L2CAP 4096
+#endif
+constexpr int kL2Cap = CUSZ_AMD_DEC_L2CAP;
 
 template <int B>
 struct LdsTables {
