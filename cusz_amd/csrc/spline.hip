@@ -31,8 +31,18 @@ namespace {
 
 constexpr int kSX = 33, kSY = 9, kSZ = 9, kSN = kSX * kSY * kSZ;  // 2673
 constexpr int kSplThreads = 256;
+constexpr int kPer = (kSN + kSplThreads - 1) / kSplThreads;  // scratch points per thread (11)
 
 __device__ __forceinline__ int sidx(int x, int y, int z) { return x + kSX * (y + kSY * z); }
+
+// a value the compiler cannot treat as loop-invariant: the prefetch's per-point coordinates are
+// then recomputed at each fetch instead of living in ~40 extra VGPRs across the whole tile loop
+__device__ __forceinline__ int opaque(int v)
+{
+  int r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
 
 struct TileInfo {
   uint32_t bx, by, bz;
@@ -74,6 +84,7 @@ template <typename T, int DIR, int U, int DX, int DY, int DZ, bool INCL, bool CO
 __device__ __forceinline__ void spl_stage(T* s, int* e, const TileInfo& t, float eb_r, float ebx2, int radius)
 {
   constexpr int N = DX * DY * DZ;
+#pragma unroll 1
   for (int q = threadIdx.x; q < N; q += kSplThreads) {
     const int ix = q % DX, iy = (q / DX) % DY, iz = q / (DX * DY);
     const int x = DIR == 2 ? U * (2 * ix + 1) : U * 2 * ix;
@@ -154,7 +165,7 @@ __device__ __forceinline__ TileInfo tile_of(uint32_t tile, uint32_t gdx, uint32_
 }
 
 template <typename T>
-__global__ void __launch_bounds__(kSplThreads) k_spline3_c(SplineArgs<T> a)
+__global__ void __launch_bounds__(kSplThreads, 4) k_spline3_c(SplineArgs<T> a)
 {
   __shared__ T s_data[kSN];
   __shared__ int s_code[kSN];
@@ -166,24 +177,43 @@ __global__ void __launch_bounds__(kSplThreads) k_spline3_c(SplineArgs<T> a)
   const uint32_t X = a.X, Y = a.Y, Z = a.Z;
   const uint32_t ax = (X + 7) / 8, ay = (Y + 7) / 8;
   const int radius = a.radius;
-  for (uint32_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+  // the next tile's 33x9x9 region is fetched into registers (kPer values per thread) while the
+  // current tile interpolates, so the load latency is not paid once per tile and row
+  T pv[kPer];
+  auto fetch = [&](uint32_t tile) {
     const TileInfo t = tile_of(tile, a.gdx, a.gdy, a.gdz, X, Y, Z);
-    // scratch: data of the 33x9x9 region (0 outside the field), anchor codes = radius
-    for (int i = tid; i < kSN; i += kSplThreads) {
+    const int ot = opaque(tid);  // recomputed per fetch, not hoisted into live registers
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      const int i = ot + k * kSplThreads;
       const int x = i % kSX, y = (i / kSX) % kSY, z = i / (kSX * kSY);
       const uint32_t gx = t.bx * 32 + x, gy = t.by * 8 + y, gz = t.bz * 8 + z;
       T v = 0;
-      if (gx < X && gy < Y && gz < Z) v = a.in[gx + (size_t)X * (gy + (size_t)Y * gz)];
-      s_data[i] = v;
-      s_code[i] = (x % 8 == 0 && y % 8 == 0 && z % 8 == 0) ? radius : 0;
+      if (i < kSN && gx < X && gy < Y && gz < Z) v = a.in[gx + (size_t)X * (gy + (size_t)Y * gz)];
+      pv[k] = v;
     }
-    // anchors: the tile's interior points on the 8-lattice (c_gather_anchor, spline3.inl:205-220)
-    if (tid < 4) {
-      const uint32_t gx = t.bx * 32 + 8 * tid, gy = t.by * 8, gz = t.bz * 8;
-      if (gx < X && gy < Y && gz < Z)
-        a.anchor[gx / 8 + ax * (gy / 8 + (size_t)ay * (gz / 8))] = a.in[gx + (size_t)X * (gy + (size_t)Y * gz)];
+  };
+  if (blockIdx.x < a.ntiles) fetch(blockIdx.x);
+  for (uint32_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    const TileInfo t = tile_of(tile, a.gdx, a.gdy, a.gdz, X, Y, Z);
+    // scratch: data of the 33x9x9 region (0 outside the field), anchor codes = radius
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      const int i = tid + k * kSplThreads;
+      if (i < kSN) {
+        const int x = i % kSX, y = (i / kSX) % kSY, z = i / (kSX * kSY);
+        s_data[i] = pv[k];
+        s_code[i] = (x % 8 == 0 && y % 8 == 0 && z % 8 == 0) ? radius : 0;
+      }
     }
     __syncthreads();
+    // anchors: the tile's interior points on the 8-lattice (c_gather_anchor, spline3.inl:205-220);
+    // no stage writes them, so they are read back from the scratch
+    if (tid < 4) {
+      const uint32_t gx = t.bx * 32 + 8 * tid, gy = t.by * 8, gz = t.bz * 8;
+      if (gx < X && gy < Y && gz < Z) a.anchor[gx / 8 + ax * (gy / 8 + (size_t)ay * (gz / 8))] = s_data[sidx(8 * tid, 0, 0)];
+    }
+    if (tile + gridDim.x < a.ntiles) fetch(tile + gridDim.x);
     spl_interpolate<T, true>(s_data, s_code, t, a.eb_r, a.ebx2, radius);
     // interior codes out (shmem2global_32x8x8data_with_compaction, spline3.inl:370-398): plane z
     // of the tile per pass, thread -> (x, y).  Outliers get their (z, y, x) rank from a count
@@ -332,7 +362,7 @@ __global__ void __launch_bounds__(256) k_spl_bucket_fill(const uint32_t* cells, 
 }
 
 template <typename T>
-__global__ void __launch_bounds__(kSplThreads) k_spline3_x(SplineXArgs<T> a)
+__global__ void __launch_bounds__(kSplThreads, 4) k_spline3_x(SplineXArgs<T> a)
 {
   __shared__ T s_data[kSN];
   __shared__ int s_code[kSN];
@@ -340,31 +370,62 @@ __global__ void __launch_bounds__(kSplThreads) k_spline3_x(SplineXArgs<T> a)
   const uint32_t X = a.X, Y = a.Y, Z = a.Z;
   const uint32_t ax = (X + 7) / 8, ay = (Y + 7) / 8, az = (Z + 7) / 8;
   const int radius = a.radius;
-  for (uint32_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+  const uint32_t* bk = a.nbucket ? (*a.unsorted ? a.bucket : a.cells) : nullptr;
+  __shared__ uint32_t s_rng[8][2];
+  // the next tile's codes, its anchors (threads 0..19, one 8-lattice point each) and the bucket
+  // ranges of it and its seven upper neighbours (threads 0..7) are fetched into registers while
+  // the current tile interpolates
+  int pc[kPer];
+  T pa = 0;
+  uint32_t pr0 = 0, pr1 = 0;
+  auto fetch = [&](uint32_t tile) {
     const TileInfo t = tile_of(tile, a.gdx, a.gdy, a.gdz, X, Y, Z);
-    // x_reset_scratch_33x9x9data + global2shmem_fuse (spline3.inl:241-278, :309-328)
-    for (int i = tid; i < kSN; i += kSplThreads) {
+    const int ot = opaque(tid);  // recomputed per fetch, not hoisted into live registers
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      const int i = ot + k * kSplThreads;
       const int x = i % kSX, y = (i / kSX) % kSY, z = i / (kSX * kSY);
       const uint32_t gx = t.bx * 32 + x, gy = t.by * 8 + y, gz = t.bz * 8 + z;
-      T v = 0;
-      if (x % 8 == 0 && y % 8 == 0 && z % 8 == 0) {
-        const uint32_t Ax = x / 8 + t.bx * 4, Ay = y / 8 + t.by, Az = z / 8 + t.bz;
-        if (Ax < ax && Ay < ay && Az < az) v = a.anchor[Ax + ax * (Ay + (size_t)ay * Az)];
-      }
-      s_data[i] = v;
       int c = 0;
-      if (gx < X && gy < Y && gz < Z) c = a.codes[gx + (size_t)X * (gy + (size_t)Y * gz)];
-      s_code[i] = c;
+      if (i < kSN && gx < X && gy < Y && gz < Z) c = a.codes[gx + (size_t)X * (gy + (size_t)Y * gz)];
+      pc[k] = c;
     }
-    __syncthreads();
-    // outlier codes of this tile and of the faces it shares with its upper neighbours
-    if (a.nbucket) {
-      for (int k = 0; k < 8; k++) {
-        const uint32_t nbx = t.bx + (k & 1), nby = t.by + ((k >> 1) & 1), nbz = t.bz + (k >> 2);
-        if (nbx >= a.gdx || nby >= a.gdy || nbz >= a.gdz) continue;
+    pa = 0;
+    if (tid < 20) {  // x_reset_scratch_33x9x9data + global2shmem_fuse (spline3.inl:241-278, :309-328)
+      const uint32_t Ax = tid % 5 + t.bx * 4, Ay = (tid / 5) % 2 + t.by, Az = tid / 10 + t.bz;
+      if (Ax < ax && Ay < ay && Az < az) pa = a.anchor[Ax + ax * (Ay + (size_t)ay * Az)];
+    }
+    pr0 = pr1 = 0;
+    if (bk && tid < 8) {
+      const uint32_t nbx = t.bx + (tid & 1), nby = t.by + ((tid >> 1) & 1), nbz = t.bz + (tid >> 2);
+      if (nbx < a.gdx && nby < a.gdy && nbz < a.gdz) {
         const uint32_t nt = nbx + a.gdx * (nby + a.gdy * nbz);
-        const uint32_t b0 = a.boff[nt], b1 = a.boff[nt + 1];
-        const uint32_t* bk = *a.unsorted ? a.bucket : a.cells;
+        pr0 = a.boff[nt], pr1 = a.boff[nt + 1];
+      }
+    }
+  };
+  if (blockIdx.x < a.ntiles) fetch(blockIdx.x);
+  for (uint32_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    const TileInfo t = tile_of(tile, a.gdx, a.gdy, a.gdz, X, Y, Z);
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      const int i = tid + k * kSplThreads;
+      if (i < kSN) {
+        const int x = i % kSX, y = (i / kSX) % kSY, z = i / (kSX * kSY);
+        if (!(x % 8 == 0 && y % 8 == 0 && z % 8 == 0)) s_data[i] = 0;
+        s_code[i] = pc[k];
+      }
+    }
+    if (tid < 20) s_data[sidx(8 * (tid % 5), 8 * ((tid / 5) % 2), 8 * (tid / 10))] = pa;
+    if (tid < 8) s_rng[tid][0] = pr0, s_rng[tid][1] = pr1;
+    __syncthreads();
+    if (tile + gridDim.x < a.ntiles) fetch(tile + gridDim.x);
+    // outlier codes of this tile and of the faces it shares with its upper neighbours
+    if (bk) {
+      bool any = false;
+      for (int k = 0; k < 8; k++) {
+        const uint32_t b0 = s_rng[k][0], b1 = s_rng[k][1];
+        any |= b1 > b0;
         for (uint32_t j = b0 + tid; j < b1; j += kSplThreads) {
           const uint32_t cv = bk[2 * j], gid = bk[2 * j + 1];
           const uint32_t gx = gid % X, gy = (gid / X) % Y, gz = gid / (X * Y);
@@ -373,7 +434,7 @@ __global__ void __launch_bounds__(kSplThreads) k_spline3_x(SplineXArgs<T> a)
             s_code[sidx(lx, ly, lz)] = (int)__builtin_bit_cast(float, cv);
         }
       }
-      __syncthreads();
+      if (any) __syncthreads();
     }
     spl_interpolate<T, false>(s_data, s_code, t, a.eb_r, a.ebx2, radius);
     for (int z = 0; z < 8; z++) {
