@@ -28,7 +28,9 @@ CASES = [
     ((256, 32, 16), np.float32, 1e-4, True, 512, "smooth"),    # ZigZag
     ((256, 32, 16), np.float64, 1e-5, True, 512, "smooth"),
     ((256, 24, 16), np.float32, 1e-3, False, 64, "smooth"),    # small radius: many outliers
-    ((256, 16, 16), np.float32, 1e-2, False, 512, "noise"),    # high entropy: HBM-read decode path
+    ((256, 16, 16), np.float32, 1e-2, False, 512, "noise"),    # high entropy: HBM-read decode path,
+    ((256, 16, 16), np.float32, 1e-2, True, 512, "noise"),     # and pass-1 byte codes escaping to u16
+    ((256, 16, 16), np.float64, 3e-2, False, 256, "noise"),
     ((256, 16, 8), np.float32, 0.5, False, 512, "int"),
 ]
 
