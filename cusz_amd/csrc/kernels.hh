@@ -155,6 +155,10 @@ struct SplineXArgs {
   const uint32_t* cells = nullptr;    // the archive's cells (already grouped: archives of this compressor)
   const uint32_t* unsorted = nullptr; // device flag: use `bucket` instead of `cells`
   size_t nbucket = 0;
+  // outlier index -> (x, y, z) by multiply-high: q = mulhi(i, m) >> s for divisors X and Y
+  // (set by the launcher; exact for i < 2^31, ndiv = false makes the kernel divide)
+  uint32_t mX = 0, sX = 0, mY = 0, sY = 0;
+  bool ndiv = true;
 };
 // cells: the archive's outlier segment ({f32 code, u32 idx} each); scratch: spline_x_scratch_words
 template <typename T>

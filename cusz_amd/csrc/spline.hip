@@ -421,14 +421,24 @@ __global__ void __launch_bounds__(kSplThreads, 4) k_spline3_x(SplineXArgs<T> a)
     __syncthreads();
     if (tile + gridDim.x < a.ntiles) fetch(tile + gridDim.x);
     // outlier codes of this tile and of the faces it shares with its upper neighbours
+#ifdef CUSZ_AMD_DIAG_NOBUCKET  // diagnostic build: outliers ignored (wrong output)
+    if (false) {
+#else
     if (bk) {
+#endif
       bool any = false;
       for (int k = 0; k < 8; k++) {
         const uint32_t b0 = s_rng[k][0], b1 = s_rng[k][1];
         any |= b1 > b0;
         for (uint32_t j = b0 + tid; j < b1; j += kSplThreads) {
           const uint32_t cv = bk[2 * j], gid = bk[2 * j + 1];
-          const uint32_t gx = gid % X, gy = (gid / X) % Y, gz = gid / (X * Y);
+          uint32_t gx, gy, gz;
+          if (a.ndiv) gx = gid % X, gy = (gid / X) % Y, gz = gid / (X * Y);
+          else {
+            const uint32_t r = __umulhi(gid, a.mX) >> a.sX;  // gid / X
+            gz = __umulhi(r, a.mY) >> a.sY;                 // r / Y
+            gx = gid - r * X, gy = r - gz * Y;
+          }
           const int lx = (int)gx - (int)(t.bx * 32), ly = (int)gy - (int)(t.by * 8), lz = (int)gz - (int)(t.bz * 8);
           if (lx >= 0 && lx < kSX && ly >= 0 && ly < kSY && lz >= 0 && lz < kSZ)
             s_code[sidx(lx, ly, lz)] = (int)__builtin_bit_cast(float, cv);
@@ -501,6 +511,17 @@ int launch_spline3_x(SplineXArgs<T> a, const uint32_t* cells, size_t ncell, uint
     a.bucket = bucket;
     a.cells = cells;
     a.unsorted = unsorted;
+  }
+  if ((size_t)a.X * a.Y * a.Z < (1ull << 31)) {
+    // d >= 2, l = ceil(log2 d): m = ceil(2^(31 + l) / d) < 2^32, i / d = (i * m) >> (31 + l)
+    auto magic = [](uint32_t d, uint32_t& m, uint32_t& sh) {
+      uint32_t l = 1;
+      while ((1ull << l) < d) l++;
+      m = (uint32_t)(((1ull << (31 + l)) + d - 1) / d);
+      sh = l - 1;
+    };
+    a.ndiv = a.X < 2 || a.Y < 2;
+    if (!a.ndiv) magic(a.X, a.mX, a.sX), magic(a.Y, a.mY, a.sY);
   }
   const int grid = spl_grid((const void*)k_spline3_x<T>, 0, a.ntiles);
   k_spline3_x<T><<<grid, kSplThreads, 0, st>>>(a);

@@ -45,7 +45,7 @@ def main():
             for k in names:
                 acc[k] += (tc[k] if k in (cz.T_EXTREMA, cz.T_PREDICT, cz.T_ENCODE, cz.T_COMPRESS) else td[k]) / a.reps
     err = (out.double() - d_in.double()).abs().max().item()
-    print(f"CR={n * d_in.element_size() / nb:.3f} err={err:.3e} eb_abs={r.header.rc.eb:.3e}")
+    print(f"CR={n * d_in.element_size() / nb:.3f} err={err:.3e} eb_abs={r.header.rc.eb:.3e} outliers={r.header.splen}")
     print(" ".join(f"{names[k]}={acc[k] * 1e3:.1f}us" for k in names))
 
 
