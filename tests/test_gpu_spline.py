@@ -115,3 +115,40 @@ def test_spline_fullsize_512(oracle):
         co, _, _, _ = oracle.spline3_c(sub, (512, 512, 9), ebx)
         np.testing.assert_array_equal(codes[z0:z0 + 8].ravel(), co.reshape(9, 512, 512)[:8].ravel())
     r.close()
+
+
+@pytest.mark.parametrize("order", ["reversed_in_tile", "shuffled"])
+def test_spline_decompress_reordered_outliers(order):
+    """Outlier cells in any order decompress identically: tile-sorted but not (z, y, x) inside a
+    tile (read as the per-tile lists directly), and fully shuffled (the bucket kernels rebuild
+    the per-tile lists)."""
+    import torch
+
+    dims, dtype, eb = (70, 19, 13), np.float32, 3e-6
+    n = int(np.prod(dims))
+    data = datagen.smooth3d_np(dims, 5, dtype=dtype)
+    r = cz.Resource(cz.F4, dims, cz.Spline)
+    d_in = to_device(data)
+    ptr, nbytes, _ = r.compress(d_in.data_ptr(), eb, cz.Abs)
+    arch = bytearray(d2h(ptr, nbytes).tobytes())
+    out0 = empty_device(n, torch.float32)
+    r.decompress(ptr, nbytes, out0.data_ptr())
+    sync()
+    h = parse_archive(bytes(arch))["header"]
+    cells = np.frombuffer(bytes(arch[h.entry[3]:h.entry[4]]), np.uint64).copy()
+    assert cells.size > 100
+    if order == "shuffled":
+        cells = cells[np.random.default_rng(1).permutation(cells.size)]
+    else:
+        gid = (cells >> np.uint64(32)).astype(np.int64)
+        gx, gy, gz = gid % dims[0], (gid // dims[0]) % dims[1], gid // (dims[0] * dims[1])
+        gdx, gdy = (dims[0] + 31) // 32, (dims[1] + 7) // 8
+        tile = gx // 32 + gdx * (gy // 8 + gdy * (gz // 8))
+        cells = cells[np.lexsort((-gid, tile))]  # tile order kept, descending inside a tile
+    arch[h.entry[3]:h.entry[4]] = cells.tobytes()
+    d_arch = torch.tensor(np.frombuffer(bytes(arch), np.uint8)).cuda()
+    out1 = empty_device(n, torch.float32)
+    r.decompress(d_arch.data_ptr(), nbytes, out1.data_ptr())
+    sync()
+    np.testing.assert_array_equal(out1.cpu().numpy().view(np.uint32), out0.cpu().numpy().view(np.uint32))
+    r.close()
