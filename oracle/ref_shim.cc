@@ -143,13 +143,20 @@ void ref_time_stages_f32(
     const float* in, size_t x, size_t y, size_t z, double eb, uint16_t radius, double* ms)
 {
   size_t n = x * y * z;
+  // The reference predicts every point of a partial tile, stale buffer contents included, and
+  // may record outliers at indices past the field (lrz.seq.inl:266-284: no boundary check before
+  // the outlier append); CPU_scatter then writes them.  Size the outlier list and the scatter
+  // target for the largest such index (x < 256-, y < 16-, z < 8-multiples) so it stays in bounds.
+  auto up = [](size_t v, size_t m) { return (v + m - 1) / m * m; };
+  const size_t ry = y == 1 ? 1 : up(y, 16), rz = z == 1 ? 1 : up(z, 8);
+  const size_t npad = up(x, 256) + ry * x + rz * x * y;
   auto codes = std::make_unique<uint16_t[]>(n);
-  auto outlier = std::make_unique<_portable::compact_CPU<f4, u4>>(n);
+  auto outlier = std::make_unique<_portable::compact_CPU<f4, u4>>(npad);
   auto hist = std::make_unique<uint32_t[]>(2 * radius);
   auto book = std::make_unique<uint32_t[]>(2 * radius);
   int rvbk_bytes = (int)phf_reverse_book_bytes(2 * radius, 4, sizeof(u2));
   auto revbook = std::make_unique<uint8_t[]>(rvbk_bytes);
-  auto xdata = std::make_unique<float[]>(n);
+  auto xdata = std::make_unique<float[]>(npad);
   psz_len len{x, y, z};
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point t0) {
@@ -171,7 +178,7 @@ void ref_time_stages_f32(
       hist.get(), 2 * radius, book.get(), revbook.get(), rvbk_bytes, nullptr);
   ms[2] = ms_since(t0);
 
-  memset(xdata.get(), 0, sizeof(float) * n);
+  memset(xdata.get(), 0, sizeof(float) * npad);
   psz::module::CPU_scatter<f4, u4>::kernel_v2(outlier->val_idx(), outlier->num(), xdata.get());
   t0 = clk::now();
   psz::module::CPU_x_lorenzo_nd<f4, false, u2>::kernel(
