@@ -21,12 +21,27 @@ int launch_lorenzo_c(const T* in, size_t lx, size_t ly, size_t lz, double eb, in
                      const LorenzoGeom& g, uint16_t* codes, const OutlierSink& ol, uint32_t* hist,
                      int bklen, hipStream_t st);
 
-template <typename T>
-int launch_lorenzo_x(const uint16_t* codes, T* out, size_t lx, size_t ly, size_t lz, double eb, int radius,
-                     bool zigzag, const LorenzoGeom& g, hipStream_t st);
+// 1-D Lorenzo (non-ZigZag) reads the outlier values straight from the archive's cells when they
+// are in strictly increasing index order (this compressor's archives without spill): code 0 marks
+// exactly the outliers, so the k-th zero code of a brick takes the brick's k-th cell.  bstart
+// (nbricks + 1) and the unsorted flag come from launch_x1d_bounds; an unsorted list falls back
+// to the scatter (launch_scatter with only_if = unsorted) and reads from `out`.
+struct X1dOutliers {
+  const uint32_t* cells = nullptr;
+  size_t ncell = 0;
+  const uint32_t* bstart = nullptr;
+  const uint32_t* unsorted = nullptr;
+};
+int launch_x1d_bounds(const uint32_t* cells, size_t ncell, size_t n, uint32_t nbricks, uint32_t* bstart,
+                      uint32_t* unsorted, hipStream_t st);
 
 template <typename T>
-int launch_scatter(const uint32_t* cells, size_t nnz, T* out, size_t n, hipStream_t st);
+int launch_lorenzo_x(const uint16_t* codes, T* out, size_t lx, size_t ly, size_t lz, double eb, int radius,
+                     bool zigzag, const LorenzoGeom& g, hipStream_t st, const X1dOutliers* ox = nullptr);
+
+template <typename T>
+int launch_scatter(const uint32_t* cells, size_t nnz, T* out, size_t n, hipStream_t st,
+                   const uint32_t* only_if = nullptr);
 
 // ---- Huffman (huffman.hip) ---------------------------------------------------------------
 struct HfEncodeArgs {

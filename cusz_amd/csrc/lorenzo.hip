@@ -252,24 +252,57 @@ __device__ __forceinline__ void fuse_row(const uint16_t* __restrict__ codes, con
 
 template <typename T, bool ZZ>
 __global__ void __launch_bounds__(256)
-k_lorenzo_x1d(const uint16_t* __restrict__ codes, T* out, size_t n, T ebx2, T r, uint32_t nbricks)
+k_lorenzo_x1d(const uint16_t* __restrict__ codes, T* out, size_t n, T ebx2, T r, uint32_t nbricks, X1dOutliers ox)
 {
   constexpr int V = 4;  // the reference thread owns 4 consecutive elements (launch.hh:124-132)
   const int lane = threadIdx.x & 63;
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  // outlier values from the sorted cells (see X1dOutliers) instead of the scattered `out`
+  const bool fused = !ZZ && ox.cells && !*ox.unsorted;
+  const uint64_t lt = (1ull << lane) - 1;
   for (uint32_t brick = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); brick < nbricks; brick += nw) {
     const size_t bbase = (size_t)brick * 16384;
     T carry = 0;
     const uint32_t x0 = lane * V;
     // pipelined row loop: codes arrive two rows ahead, the outlier values (read from `out`
-    // where the code is 0) one row ahead, so no row waits on a load it has just issued
+    // where the code is 0, or from the cells) one row ahead, so no row waits on a load it has
+    // just issued
     auto rlen = [&](size_t b0) { return (uint32_t)(n - b0 < 256 ? n - b0 : 256); };
+    size_t cp = fused ? ox.bstart[brick] : 0;  // next cell of this brick
+    auto outliers = [&](const uint16_t (&c)[V], size_t b0, T (&o)[V]) {
+      const uint32_t len = rlen(b0);
+      if (!fused) {
+#pragma unroll
+        for (int k = 0; k < V; k++) o[k] = (x0 + k < len && c[k] == 0) ? out[b0 + x0 + k] : T(0);
+        return;
+      }
+      // rank of each zero code in (lane, k) = index order: zeros of lower lanes, then of lower k
+      bool z[V];
+      uint32_t below = 0, tot = 0;
+#pragma unroll
+      for (int k = 0; k < V; k++) {
+        z[k] = x0 + k < len && c[k] == 0;
+        const uint64_t m = __ballot(z[k]);
+        below += __popcll(m & lt), tot += __popcll(m);
+      }
+      uint32_t rank = below;
+#pragma unroll
+      for (int k = 0; k < V; k++) {
+        T v = 0;
+        if (z[k]) {
+          const size_t j = cp + rank;
+          if (j < ox.ncell) v = (T)__builtin_bit_cast(float, ox.cells[2 * j]);
+          rank++;
+        }
+        o[k] = v;
+      }
+      cp += tot;
+    };
     uint16_t c1[V], c2[V];
     T o1[V];
     load_codes<V>(codes, bbase, x0, rlen(bbase), true, c1);
     if (bbase + 256 < n) load_codes<V>(codes, bbase + 256, x0, rlen(bbase + 256), true, c2);
-#pragma unroll
-    for (int k = 0; k < V; k++) o1[k] = (x0 + k < rlen(bbase) && c1[k] == 0) ? out[bbase + x0 + k] : T(0);
+    outliers(c1, bbase, o1);
     for (int s = 0; s < 64; s++) {
       const size_t base = bbase + (size_t)s * 256;
       if (base >= n) break;
@@ -281,10 +314,8 @@ k_lorenzo_x1d(const uint16_t* __restrict__ codes, T* out, size_t n, T ebx2, T r,
       const size_t b1 = base + 256, b2 = base + 512;
       if (s < 63 && b1 < n) {
 #pragma unroll
-        for (int k = 0; k < V; k++) {
-          c1[k] = c2[k];
-          o1[k] = (x0 + k < rlen(b1) && c1[k] == 0) ? out[b1 + x0 + k] : T(0);
-        }
+        for (int k = 0; k < V; k++) c1[k] = c2[k];
+        outliers(c1, b1, o1);
         if (s < 62 && b2 < n) load_codes<V>(codes, b2, x0, rlen(b2), true, c2);
       }
       T b[V];
@@ -447,11 +478,33 @@ k_lorenzo_x3d(const uint16_t* __restrict__ codes, T* out, uint32_t lx, uint32_t 
 // the archive (read as two u32).
 template <typename T>
 __global__ void __launch_bounds__(256)
-k_scatter(const uint32_t* __restrict__ cells, size_t nnz, T* out, size_t n)
+k_scatter(const uint32_t* __restrict__ cells, size_t nnz, T* out, size_t n, const uint32_t* only_if)
 {
+  if (only_if && !*only_if) return;  // the 1-D reconstruction reads the sorted cells itself
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nnz; i += (size_t)gridDim.x * blockDim.x) {
     const uint32_t vb = cells[2 * i], idx = cells[2 * i + 1];
     if (idx < n) out[idx] = (T)__builtin_bit_cast(float, vb);
+  }
+}
+
+// first cell of every 1-D brick (16384 elements) and whether the cells are strictly increasing
+// (bstart and *unsorted zeroed before)
+__global__ void __launch_bounds__(256) k_x1d_bounds(const uint32_t* __restrict__ cells, size_t ncell, size_t n,
+                                                    uint32_t nbricks, uint32_t* bstart, uint32_t* unsorted)
+{
+  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < ncell; i += (size_t)gridDim.x * 256) {
+    const uint32_t idx = cells[2 * i + 1];
+    const int64_t b = idx < n ? (int64_t)(idx / 16384) : (int64_t)nbricks;
+    int64_t bp = -1;
+    if (i > 0) {
+      const uint32_t ip = cells[2 * i - 1];
+      if (ip >= idx) atomicOr(unsorted, 1u);
+      bp = ip < n ? (int64_t)(ip / 16384) : (int64_t)nbricks;
+    }
+    if (idx >= n) atomicOr(unsorted, 1u);
+    for (int64_t u = bp + 1; u <= b && u <= (int64_t)nbricks; u++) bstart[u] = (uint32_t)i;
+    if (i + 1 == ncell)
+      for (int64_t u = b + 1; u <= (int64_t)nbricks; u++) bstart[u] = (uint32_t)ncell;
   }
 }
 
@@ -529,16 +582,17 @@ int launch_lorenzo_c(const T* in, size_t lx, size_t ly, size_t lz, double eb, in
 
 template <typename T>
 int launch_lorenzo_x(const uint16_t* codes, T* out, size_t lx, size_t ly, size_t lz, double eb, int radius,
-                     bool zigzag, const LorenzoGeom& g, hipStream_t st)
+                     bool zigzag, const LorenzoGeom& g, hipStream_t st, const X1dOutliers* ox)
 {
   const T ebx2 = (T)(eb * 2);  // lrz_x.cuhip.inl:432
   const T r = (T)radius;
   const int grid = grid_for(g.nbricks);
   if (g.ndim == 1) {
+    const X1dOutliers o = ox ? *ox : X1dOutliers{};
     if (zigzag)
-      k_lorenzo_x1d<T, true><<<grid, 256, 0, st>>>(codes, out, lx, ebx2, r, g.nbricks);
+      k_lorenzo_x1d<T, true><<<grid, 256, 0, st>>>(codes, out, lx, ebx2, r, g.nbricks, o);
     else
-      k_lorenzo_x1d<T, false><<<grid, 256, 0, st>>>(codes, out, lx, ebx2, r, g.nbricks);
+      k_lorenzo_x1d<T, false><<<grid, 256, 0, st>>>(codes, out, lx, ebx2, r, g.nbricks, o);
   }
   else if (g.ndim == 2) {
     DISPATCH_V(g.V, if (zigzag) k_lorenzo_x2d<T, VV, true><<<grid, 256, 0, st>>>(
@@ -556,12 +610,22 @@ int launch_lorenzo_x(const uint16_t* codes, T* out, size_t lx, size_t ly, size_t
 }
 
 template <typename T>
-int launch_scatter(const uint32_t* cells, size_t nnz, T* out, size_t n, hipStream_t st)
+int launch_scatter(const uint32_t* cells, size_t nnz, T* out, size_t n, hipStream_t st, const uint32_t* only_if)
 {
   if (nnz == 0) return 0;
   uint32_t grid = cdiv(nnz, 256);
   if (grid > 4096) grid = 4096;
-  k_scatter<T><<<grid, 256, 0, st>>>(cells, nnz, out, n);
+  k_scatter<T><<<grid, 256, 0, st>>>(cells, nnz, out, n, only_if);
+  return (int)hipGetLastError();
+}
+
+int launch_x1d_bounds(const uint32_t* cells, size_t ncell, size_t n, uint32_t nbricks, uint32_t* bstart,
+                      uint32_t* unsorted, hipStream_t st)
+{
+  if (ncell == 0) return 0;
+  uint32_t grid = cdiv(ncell, 256);
+  if (grid > 4096) grid = 4096;
+  k_x1d_bounds<<<grid, 256, 0, st>>>(cells, ncell, n, nbricks, bstart, unsorted);
   return (int)hipGetLastError();
 }
 
@@ -572,10 +636,10 @@ template int launch_lorenzo_c<double>(const double*, size_t, size_t, size_t, dou
                                       const LorenzoGeom&, uint16_t*, const OutlierSink&, uint32_t*, int,
                                       hipStream_t);
 template int launch_lorenzo_x<float>(const uint16_t*, float*, size_t, size_t, size_t, double, int, bool,
-                                     const LorenzoGeom&, hipStream_t);
+                                     const LorenzoGeom&, hipStream_t, const X1dOutliers*);
 template int launch_lorenzo_x<double>(const uint16_t*, double*, size_t, size_t, size_t, double, int, bool,
-                                      const LorenzoGeom&, hipStream_t);
-template int launch_scatter<float>(const uint32_t*, size_t, float*, size_t, hipStream_t);
-template int launch_scatter<double>(const uint32_t*, size_t, double*, size_t, hipStream_t);
+                                      const LorenzoGeom&, hipStream_t, const X1dOutliers*);
+template int launch_scatter<float>(const uint32_t*, size_t, float*, size_t, hipStream_t, const uint32_t*);
+template int launch_scatter<double>(const uint32_t*, size_t, double*, size_t, hipStream_t, const uint32_t*);
 
 }  // namespace cusz_amd

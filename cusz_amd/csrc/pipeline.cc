@@ -91,6 +91,7 @@ struct Pipeline {
   uint32_t* d_spl_off = nullptr;
   uint32_t* d_spl_sps = nullptr;  // per-tile spill range starts
   uint32_t* d_spl_x = nullptr;    // decompression buckets
+  uint32_t* d_x1d = nullptr;      // 1-D decompression: per-brick first outlier cell + unsorted flag
   size_t spl_x_words = 0;
   int sublen = 256, pardeg = 1;
   int user_sublen = 0;
@@ -147,7 +148,7 @@ struct Pipeline {
     for (void* p : {(void*)d_codes, (void*)d_hist, (void*)d_book, (void*)d_slots, (void*)d_brick_cnt,
                     (void*)d_brick_off, (void*)d_spill, (void*)d_small, (void*)d_status, (void*)d_archive,
                     (void*)d_enc_temp, (void*)d_spl_slots, (void*)d_spl_cnt, (void*)d_spl_off, (void*)d_spl_x, (void*)d_spl_sps,
-                    (void*)d_bhist, (void*)d_ub, (void*)d_bbase, (void*)d_plan})
+                    (void*)d_bhist, (void*)d_ub, (void*)d_bbase, (void*)d_plan, (void*)d_x1d})
       if (p) (void)hipFree(p);
     if (h_xfer) (void)hipHostFree(h_xfer);
     for (auto& e : ev)
@@ -155,7 +156,7 @@ struct Pipeline {
     d_codes = nullptr, d_hist = nullptr, d_book = nullptr, d_slots = nullptr, d_brick_cnt = nullptr;
     d_brick_off = nullptr, d_spill = nullptr, d_small = nullptr, d_status = nullptr, d_archive = nullptr;
     d_enc_temp = nullptr;
-    d_bhist = nullptr, d_ub = nullptr, d_bbase = nullptr, d_plan = nullptr;
+    d_bhist = nullptr, d_ub = nullptr, d_bbase = nullptr, d_plan = nullptr, d_x1d = nullptr;
     d_spl_slots = nullptr, d_spl_cnt = nullptr, d_spl_off = nullptr, d_spl_x = nullptr, d_spl_sps = nullptr;
     spl_slot_cells = 0, spl_x_words = 0;
     h_xfer = nullptr;
@@ -192,6 +193,7 @@ struct Pipeline {
     CUSZ_AMD_HIP_CHECK(hipGetDevice(&device));
     tune_chunking(n, device, &sublen, &pardeg);
     geom = lorenzo_geom(ndim, l.x, l.y, l.z, elem_bytes);
+    if (ndim == 1) CUSZ_AMD_HIP_CHECK(hipMalloc(&d_x1d, ((size_t)geom.nbricks + 2) * 4));
     sgeom = spline_geom(l.x, l.y, l.z);
     spl_cap = (uint32_t)(std::min<size_t>(l.x, 32) * std::min<size_t>(l.y, 8) * std::min<size_t>(l.z, 8) / 10 + 16);
     // outlier capacity: 10 % of the input like the reference (buf_comp.hh:55), as per-brick
@@ -613,17 +615,24 @@ struct Pipeline {
     if (h->len.x != len.x || h->len.y != len.y || h->len.z != len.z) return PSZ_ABORT_UNSUPPORTED_DIMENSION;
     if (pred == Spline) return decompress_spline<T>(h, in, out);
     mark(6);
+    const bool brickdec = bl.g.ok && decoder == 0 && h->vle_sublen == bl.g.W && 2 * h->rc.radius <= kMaxBklen;
+    const uint32_t* cells = reinterpret_cast<const uint32_t*>(in + h->entry[PSZHEADER_SPFMT]);
+    X1dOutliers ox;  // 1-D: the reconstruction reads sorted cells directly (no scatter pass)
+    if (geom.ndim == 1 && d_x1d && !zz && !brickdec && h->splen) {
+      const uint32_t nb = geom.nbricks;
+      CUSZ_AMD_HIP_CHECK(hipMemsetAsync(d_x1d, 0, ((size_t)nb + 2) * 4, stream));
+      CUSZ_AMD_HIP_CHECK((hipError_t)launch_x1d_bounds(cells, h->splen, n, nb, d_x1d, d_x1d + nb + 1, stream));
+      ox = X1dOutliers{cells, (size_t)h->splen, d_x1d, d_x1d + nb + 1};
+    }
     if (zz) CUSZ_AMD_HIP_CHECK(hipMemsetAsync(out, 0, n * sizeof(T), stream));
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_scatter<T>(
-        reinterpret_cast<const uint32_t*>(in + h->entry[PSZHEADER_SPFMT]), h->splen, out, n, stream));
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_scatter<T>(cells, h->splen, out, n, stream, ox.unsorted));
     mark(7);
-    if (bl.g.ok && decoder == 0 && h->vle_sublen == bl.g.W && 2 * h->rc.radius <= kMaxBklen)
-      return decompress_brick<T>(h, in, out, zz);
+    if (brickdec) return decompress_brick<T>(h, in, out, zz);
     int s = decode_codes(h, in);
     if (s) return s;
     mark(8);
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_lorenzo_x<T>(d_codes, out, len.x, len.y, len.z, h->rc.eb, h->rc.radius,
-                                                       zz, geom, stream));
+                                                       zz, geom, stream, ox.cells ? &ox : nullptr));
     mark(9);
     return PSZ_SUCCESS;
   }
