@@ -17,6 +17,7 @@
 //    self-synchronisation; a 4096-entry LDS table resolves up to two codewords per lookup;
 //    cells and output are staged in LDS so HBM sees coalesced reads and 16-B writes.
 #include "common.hh"
+#include "hf_device.hh"
 #include "kernels.hh"
 
 namespace cusz_amd {
@@ -157,7 +158,26 @@ __global__ void __launch_bounds__(64 * kPackWaves) k_hf_pack(HfEncodeArgs a, int
         bits += w[i] >> 27;
       }
       const uint32_t inc = wave_incl_scan(bits, lane);
-      if (mine) pack_words<kRound>(cells, nbits + inc - bits, w, mine);
+      // full rounds whose 4-code groups each fit 64 bits (every lane): Horner-pack each group and
+      // OR it in (hf_device.hh pack4_or); otherwise the general word-by-word packer
+      uint32_t lg[kRound / 4];
+      bool fast = mine == kRound;
+#pragma unroll
+      for (int g = 0; g < kRound / 4; g++) {
+        lg[g] = (w[4 * g] >> 27) + (w[4 * g + 1] >> 27) + (w[4 * g + 2] >> 27) + (w[4 * g + 3] >> 27);
+        fast = fast && lg[g] <= 64u;
+      }
+      if (__builtin_expect(__ballot(!fast) == 0, 1)) {
+        uint32_t p = nbits + inc - bits;
+#pragma unroll
+        for (int g = 0; g < kRound / 4; g++) {
+          const uint32_t wg[4] = {w[4 * g], w[4 * g + 1], w[4 * g + 2], w[4 * g + 3]};
+          hfd::pack4_or(cells, p, wg, lg[g]);
+          p += lg[g];
+        }
+      }
+      else if (mine)
+        pack_words<kRound>(cells, nbits + inc - bits, w, mine);
       nbits += __shfl(inc, 63);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
