@@ -124,11 +124,18 @@ __global__ void __launch_bounds__(256) k_outlier_copy(OutlierCopyArgs a, uint32_
     const uint32_t cnt = min(all, a.cap_per_brick);
     const uint64_t* src = a.slots + (size_t)brick * a.cap_per_brick;
     uint32_t* d = dst + 2ull * a.brick_off[brick];
-    for (uint32_t i = threadIdx.x & 63; i < cnt; i += 64) {
-      const uint64_t c = src[i];
-      d[2 * i] = (uint32_t)c;
-      d[2 * i + 1] = (uint32_t)(c >> 32);
+    if ((reinterpret_cast<uintptr_t>(d) & 7) == 0) {  // the archive offset decides (wave-uniform)
+      uint64_t* d8 = reinterpret_cast<uint64_t*>(d);
+#pragma unroll 4
+      for (uint32_t i = threadIdx.x & 63; i < cnt; i += 64) d8[i] = src[i];
     }
+    else
+#pragma unroll 4
+      for (uint32_t i = threadIdx.x & 63; i < cnt; i += 64) {
+        const uint64_t c = src[i];
+        d[2 * i] = (uint32_t)c;
+        d[2 * i + 1] = (uint32_t)(c >> 32);
+      }
     if (a.spill_start && all > cnt) {  // this brick's contiguous spill range follows its slot
       const uint32_t s0 = a.spill_start[brick];
       for (uint32_t i = threadIdx.x & 63; i < all - cnt; i += 64) {
