@@ -419,8 +419,8 @@ __global__ void __launch_bounds__(kSplThreads, 4) k_spline3_x(SplineXArgs<T> a)
     if (tid < 20) s_data[sidx(8 * (tid % 5), 8 * ((tid / 5) % 2), 8 * (tid / 10))] = pa;
     if (tid < 8) s_rng[tid][0] = pr0, s_rng[tid][1] = pr1;
     __syncthreads();
-    if (tile + gridDim.x < a.ntiles) fetch(tile + gridDim.x);
-    // outlier codes of this tile and of the faces it shares with its upper neighbours
+    // outlier codes of this tile and of the faces it shares with its upper neighbours (before the
+    // next tile's prefetch: waiting on these loads must not also wait on the prefetch)
 #ifdef CUSZ_AMD_DIAG_NOBUCKET  // diagnostic build: outliers ignored (wrong output)
     if (false) {
 #else
@@ -446,6 +446,7 @@ __global__ void __launch_bounds__(kSplThreads, 4) k_spline3_x(SplineXArgs<T> a)
       }
       if (any) __syncthreads();
     }
+    if (tile + gridDim.x < a.ntiles) fetch(tile + gridDim.x);
     spl_interpolate<T, false>(s_data, s_code, t, a.eb_r, a.ebx2, radius);
     for (int z = 0; z < 8; z++) {
       const int x = tid & 31, y = tid >> 5;
