@@ -371,13 +371,26 @@ __global__ void __launch_bounds__(kSplThreads, 4) k_spline3_x(SplineXArgs<T> a)
   const uint32_t ax = (X + 7) / 8, ay = (Y + 7) / 8, az = (Z + 7) / 8;
   const int radius = a.radius;
   const uint32_t* bk = a.nbucket ? (*a.unsorted ? a.bucket : a.cells) : nullptr;
-  __shared__ uint32_t s_rng[8][2];
-  // the next tile's codes, its anchors (threads 0..19, one 8-lattice point each) and the bucket
-  // ranges of it and its seven upper neighbours (threads 0..7) are fetched into registers while
-  // the current tile interpolates
+  // bucket ranges [b0, b1) of a tile and its seven upper neighbours, double-buffered by tile parity
+  __shared__ uint32_t s_rng[2][8][2];
+  // The next tile's codes and anchors (threads 0..19, one 8-lattice point each), the bucket ranges
+  // of the tile after it (threads 0..7) and the next tile's first kEnt * 256 bucket entries are
+  // fetched into registers while the current tile interpolates.
+  constexpr int kEnt = 3;
   int pc[kPer];
   T pa = 0;
   uint32_t pr0 = 0, pr1 = 0;
+  uint32_t pcv[kEnt], pgid[kEnt], pm = 0;
+  auto ranges_of = [&](uint32_t tile, uint32_t& r0, uint32_t& r1) {
+    r0 = r1 = 0;
+    if (!bk || tid >= 8 || tile >= a.ntiles) return;
+    const TileInfo t = tile_of(tile, a.gdx, a.gdy, a.gdz, X, Y, Z);
+    const uint32_t nbx = t.bx + (tid & 1), nby = t.by + ((tid >> 1) & 1), nbz = t.bz + (tid >> 2);
+    if (nbx < a.gdx && nby < a.gdy && nbz < a.gdz) {
+      const uint32_t nt = nbx + a.gdx * (nby + a.gdy * nbz);
+      r0 = a.boff[nt], r1 = a.boff[nt + 1];
+    }
+  };
   auto fetch = [&](uint32_t tile) {
     const TileInfo t = tile_of(tile, a.gdx, a.gdy, a.gdz, X, Y, Z);
     const int ot = opaque(tid);  // recomputed per fetch, not hoisted into live registers
@@ -395,17 +408,52 @@ __global__ void __launch_bounds__(kSplThreads, 4) k_spline3_x(SplineXArgs<T> a)
       const uint32_t Ax = tid % 5 + t.bx * 4, Ay = (tid / 5) % 2 + t.by, Az = tid / 10 + t.bz;
       if (Ax < ax && Ay < ay && Az < az) pa = a.anchor[Ax + ax * (Ay + (size_t)ay * Az)];
     }
-    pr0 = pr1 = 0;
-    if (bk && tid < 8) {
-      const uint32_t nbx = t.bx + (tid & 1), nby = t.by + ((tid >> 1) & 1), nbz = t.bz + (tid >> 2);
-      if (nbx < a.gdx && nby < a.gdy && nbz < a.gdz) {
-        const uint32_t nt = nbx + a.gdx * (nby + a.gdy * nbz);
-        pr0 = a.boff[nt], pr1 = a.boff[nt + 1];
+    ranges_of(tile + gridDim.x, pr0, pr1);
+  };
+  // entry e of the concatenated ranges of buffer `buf` -> its cell index (false past the end)
+  auto locate = [&](int buf, uint32_t e, uint32_t& j) {
+    uint32_t pre = 0;
+    bool found = false;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t b0 = s_rng[buf][k][0], len = s_rng[buf][k][1] - b0;
+      if (!found && e < pre + len) j = b0 + (e - pre), found = true;
+      pre += len;
+    }
+    return found;
+  };
+  auto entries = [&](int buf) {  // registers <- the first kEnt * 256 entries
+    pm = 0;
+#pragma unroll
+    for (int m = 0; m < kEnt; m++) {
+      uint32_t j;
+      if (locate(buf, (uint32_t)tid + kSplThreads * m, j)) {
+        pcv[m] = bk[2 * j], pgid[m] = bk[2 * j + 1];
+        pm |= 1u << m;
       }
     }
   };
-  if (blockIdx.x < a.ntiles) fetch(blockIdx.x);
-  for (uint32_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+  auto put = [&](const TileInfo& t, uint32_t cv, uint32_t gid) {
+    uint32_t gx, gy, gz;
+    if (a.ndiv) gx = gid % X, gy = (gid / X) % Y, gz = gid / (X * Y);
+    else {
+      const uint32_t r = __umulhi(gid, a.mX) >> a.sX;  // gid / X
+      gz = __umulhi(r, a.mY) >> a.sY;                 // r / Y
+      gx = gid - r * X, gy = r - gz * Y;
+    }
+    const int lx = (int)gx - (int)(t.bx * 32), ly = (int)gy - (int)(t.by * 8), lz = (int)gz - (int)(t.bz * 8);
+    if (lx >= 0 && lx < kSX && ly >= 0 && ly < kSY && lz >= 0 && lz < kSZ)
+      s_code[sidx(lx, ly, lz)] = (int)__builtin_bit_cast(float, cv);
+  };
+  int par = 0;
+  if (blockIdx.x < a.ntiles) {
+    ranges_of(blockIdx.x, pr0, pr1);
+    if (tid < 8) s_rng[0][tid][0] = pr0, s_rng[0][tid][1] = pr1;
+    fetch(blockIdx.x);
+    __syncthreads();
+    if (bk) entries(0);
+  }
+  for (uint32_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x, par ^= 1) {
     const TileInfo t = tile_of(tile, a.gdx, a.gdy, a.gdz, X, Y, Z);
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
@@ -417,36 +465,30 @@ __global__ void __launch_bounds__(kSplThreads, 4) k_spline3_x(SplineXArgs<T> a)
       }
     }
     if (tid < 20) s_data[sidx(8 * (tid % 5), 8 * ((tid / 5) % 2), 8 * (tid / 10))] = pa;
-    if (tid < 8) s_rng[tid][0] = pr0, s_rng[tid][1] = pr1;
+    if (tid < 8) s_rng[par ^ 1][tid][0] = pr0, s_rng[par ^ 1][tid][1] = pr1;  // the next tile's
     __syncthreads();
-    // outlier codes of this tile and of the faces it shares with its upper neighbours (before the
-    // next tile's prefetch: waiting on these loads must not also wait on the prefetch)
+    // outlier codes of this tile and of the faces it shares with its upper neighbours: the
+    // prefetched entries, then (rarely) the ones past kEnt * 256 straight from the buckets
 #ifdef CUSZ_AMD_DIAG_NOBUCKET  // diagnostic build: outliers ignored (wrong output)
     if (false) {
 #else
     if (bk) {
 #endif
-      bool any = false;
-      for (int k = 0; k < 8; k++) {
-        const uint32_t b0 = s_rng[k][0], b1 = s_rng[k][1];
-        any |= b1 > b0;
-        for (uint32_t j = b0 + tid; j < b1; j += kSplThreads) {
-          const uint32_t cv = bk[2 * j], gid = bk[2 * j + 1];
-          uint32_t gx, gy, gz;
-          if (a.ndiv) gx = gid % X, gy = (gid / X) % Y, gz = gid / (X * Y);
-          else {
-            const uint32_t r = __umulhi(gid, a.mX) >> a.sX;  // gid / X
-            gz = __umulhi(r, a.mY) >> a.sY;                 // r / Y
-            gx = gid - r * X, gy = r - gz * Y;
-          }
-          const int lx = (int)gx - (int)(t.bx * 32), ly = (int)gy - (int)(t.by * 8), lz = (int)gz - (int)(t.bz * 8);
-          if (lx >= 0 && lx < kSX && ly >= 0 && ly < kSY && lz >= 0 && lz < kSZ)
-            s_code[sidx(lx, ly, lz)] = (int)__builtin_bit_cast(float, cv);
-        }
+      uint32_t total = 0;
+      for (int k = 0; k < 8; k++) total += s_rng[par][k][1] - s_rng[par][k][0];
+#pragma unroll
+      for (int m = 0; m < kEnt; m++)
+        if ((pm >> m) & 1u) put(t, pcv[m], pgid[m]);
+      for (uint32_t e = (uint32_t)tid + kSplThreads * kEnt; e < total; e += kSplThreads) {
+        uint32_t j;
+        if (locate(par, e, j)) put(t, bk[2 * j], bk[2 * j + 1]);
       }
-      if (any) __syncthreads();
+      if (total) __syncthreads();
     }
-    if (tile + gridDim.x < a.ntiles) fetch(tile + gridDim.x);
+    if (tile + gridDim.x < a.ntiles) {
+      fetch(tile + gridDim.x);
+      if (bk) entries(par ^ 1);
+    }
     spl_interpolate<T, false>(s_data, s_code, t, a.eb_r, a.ebx2, radius);
     for (int z = 0; z < 8; z++) {
       const int x = tid & 31, y = tid >> 5;
