@@ -2,20 +2,30 @@
 """bench.py -- device-resident compress+decompress throughput of cusz_amd on MI355X.
 
 Metric (BASELINE.json): "device-resident compress+decompress GB/s (input bytes),
-512^3 f32 abs eb=1e-4".  One step = psz_compress_float + psz_decompress_float of one
-512^3 f32 field already resident in HBM (config 2 of BASELINE.json: Lorenzo-3D + histogram
-+ Huffman), through the C-ABI.  value = (bytes of input processed by all ranks) / time.
+512^3 f32 abs eb=1e-4".  One step = compress + decompress of ONE 512^3 f32 field already
+resident in HBM (config 2 of BASELINE.json: Lorenzo-3D + histogram + Huffman), through the
+C-ABI.  value = field bytes / step time (max over ranks).
 
-Multi-GPU (torchrun, one rank per GPU): every rank compresses and decompresses its own
-512^3 field (the path shards by independent fields / tile-aligned slabs, no data-path
-collective) -> "scaling": "weak"; barrier + synchronize bracket the timed steps and the
-max time over ranks is used.
+GPUs (one process per GPU).  `--gpus N` with N > 1 and no WORLD_SIZE in the environment
+re-launches this script under torch.distributed.run (before any GPU call in the parent); under
+torchrun WORLD_SIZE must equal N.  With N ranks the ONE field is split into tile-aligned z-slabs
+(8-plane multiples, shard.plan_slabs) -- strong scaling -- and a step is the sharded compress of
+SURVEY.md §8e:
+  pass 1 per slab (psz_amd_compress_scan_float) -> ONE all-reduce of the u32[1024] histogram
+  (RCCL) -> finish per slab with the shared codebook (psz_amd_compress_finish) -> gather of the
+  per-rank archives to rank 0 (exact-size grouped ncclSend/ncclRecv over xGMI) -> every rank
+  decompresses its own slab.
+The root merges the gathered slabs into the whole field's archive (psz_amd_merge_archives) once,
+after timing, and checks that it decompresses within the error bound.  N = 1 is the same step
+with no collective.  Barrier + synchronize bracket the timed steps; the max time over ranks is
+used.
 
 Extra fields on the JSON line:
   roofline      dominant kernel: algorithmic bytes / its HIP-event duration vs 8 TB/s
   cpu_baseline  the reference's own CPU path (compiled from /root/reference into
-                oracle/_ref; single thread) timed on this host on the same 512^3 field
-  stages_ms     per-stage device times of the last step (HIP events in the library)
+                oracle/_ref; 1 thread, plus an all-core variant) timed on this host, N = 1 only
+  stages_ms     per-stage device times (HIP events in the library), rank 0
+  phases_ms     per-step host-clock split: compress (incl. all-reduce), gather, decompress
 """
 from __future__ import annotations
 
@@ -53,31 +63,123 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (PCIe) path timing")
     ap.add_argument("--profile-only", action="store_true", help="few steps, no baselines (rocprof)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: exercise the launch, rank plumbing and the collectives (gloo) only")
     return ap.parse_args()
 
 
-def main():
+def spawn(args) -> int:
+    """One process per GPU: re-run this script under torch.distributed.run.  Called before
+    anything in this process touches the GPU (a child process, never an exec)."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
+def main() -> int:
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn(args)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+    if args.dry_run:
+        return dry_run(args, world, rank)
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    try:
+        if args.config == 4:
+            bench_sharded(args, world, rank, dist, dev)
+        else:
+            bench_field(args, world, rank, dist, dev)
+    finally:
+        if dist is not None:
+            dist.destroy_process_group()
+    return 0
+
+
+def dry_run(args, world, rank) -> int:
+    """CPU rehearsal of the multi-rank step: gloo process group, the histogram all-reduce and the
+    exact-size gather to the root of the GPU path (cusz_amd.shard), on stand-in tensors."""
+    import torch
+
+    from cusz_amd import shard
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")
+    slab = shard.plan_slabs((512, 512, 512), world)[rank]
+    hist = torch.full((1, 1024), slab.count // 1024, dtype=torch.int64)
+    if dist is not None:
+        shard.allreduce_histograms(hist, dist)
+    part = torch.full((1000 + 7 * rank,), rank, dtype=torch.uint8)
+    got = shard.gather_to_root(part, dist, 0) if dist is not None else [part]
+    ok = int(hist.sum().item()) == 1024 * sum(s.count // 1024 for s in shard.plan_slabs((512, 512, 512), world))
+    if rank == 0:
+        ok = ok and [g.numel() for g in got] == [1000 + 7 * r for r in range(world)]
+        print(json.dumps({"metric": METRICS[args.config], "value": None, "unit": "GB/s", "n_gpus": world,
+                          "steps": 0, "warmup": 0, "dry_run": True, "collectives_ok": bool(ok),
+                          "slab_planes": [s.dims[2] for s in shard.plan_slabs((512, 512, 512), world)]}),
+              flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0 if ok else 1
+
+
+class _DevBytes:
+    """Zero-copy view of a device archive (raw pointer from psz_compress_*) for torch."""
+
+    def __init__(self, ptr: int, nbytes: int):
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False),
+                                         "version": 2, "strides": None}
+
+
+def archive_view(ptr, nbytes, dev, scratch):
+    """The archive as a uint8 tensor for RCCL: zero-copy when torch accepts the array interface,
+    else a device-to-device copy into `scratch` (resized on demand)."""
+    import torch
+
+    import cusz_amd as cz
+
+    try:
+        t = torch.as_tensor(_DevBytes(ptr, nbytes), device=dev)
+        if t.data_ptr() == ptr:
+            return t, scratch
+    except Exception:
+        pass
+    if scratch is None or scratch.numel() < nbytes:
+        scratch = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    cz.hip_memcpy(scratch.data_ptr(), ptr, nbytes, 3)
+    return scratch[:nbytes], scratch
+
+
+def bench_field(args, world, rank, dist, dev):
     import numpy as np
     import torch
 
     import cusz_amd as cz
-    from cusz_amd import datagen
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
-    if dist:
-        import torch.distributed as tdist
-
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl")
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
-    if args.config == 4:
-        return bench_sharded(args, world, rank, dist, dev)
+    from cusz_amd import datagen, shard
 
     cfg = {1: ("3600x1800", 1e-4, cz.Abs, cz.Lorenzo, torch.float32),
            2: ("512x512x512", 1e-4, cz.Abs, cz.Lorenzo, torch.float32),
@@ -88,29 +190,64 @@ def main():
     args.eb = args.eb if args.eb is not None else cfg[1]
     mode, predictor, tdt = cfg[2], cfg[3], cfg[4]
     esz = 8 if tdt == torch.float64 else 4
-    n = dims[0] * dims[1] * dims[2]
-    nbytes_in = esz * n
+    n_full = dims[0] * dims[1] * dims[2]
+    # the spline archive has an anchor segment the slab merge does not rebase: with several
+    # ranks, config 5 runs one independent field per rank (weak scaling) instead
+    sharded = world > 1 and predictor != cz.Spline
+    weak = world > 1 and not sharded
+    slab = shard.plan_slabs(dims, world)[rank] if sharded else shard.Slab(rank, 0, dims, 0)
+    my_dims, n = slab.dims, slab.count
+    seed = {1: 1, 2: 2, 3: 3, 5: 5}[args.config] + (rank if weak else 0)
 
     if args.config == 1:
-        d_in = torch.from_numpy(datagen.cesm2d_np(dims[:2], seed=1 + rank)).to(dev)
+        d_full = torch.from_numpy(datagen.cesm2d_np(dims[:2], seed=seed)).to(dev)
     elif args.config == 3:
-        d_in = datagen.hacc1d_torch(n, seed=3 + rank, device=dev)
+        d_full = datagen.hacc1d_torch(n_full, seed=seed, device=dev)
     else:
-        d_in = datagen.smooth3d_torch(dims, seed=(5 if args.config == 5 else 2) + rank, dtype=tdt, device=dev)
+        d_full = datagen.smooth3d_torch(dims, seed=seed, dtype=tdt, device=dev)
+    d_in = d_full[slab.offset:slab.offset + n].clone() if sharded else d_full
+    if sharded and rank != 0:
+        del d_full  # the root keeps the whole field to validate the merged archive
     d_out = torch.empty(n, dtype=tdt, device=dev)
     stream = torch.cuda.current_stream(dev)
-    r = cz.Resource(cz.F4 if esz == 4 else cz.F8, dims, predictor, stream=stream.cuda_stream)
-    r.enable_timing(True)
+    r = cz.Resource(cz.F4 if esz == 4 else cz.F8, my_dims, predictor, stream=stream.cuda_stream)
+    hist = torch.empty(2 * 512, dtype=torch.int32, device=dev)
+    mm = torch.empty(2, dtype=torch.float64, device=dev)
+    nbytes_in = esz * n  # this rank's bytes
+    total_bytes = esz * n_full * (world if weak else 1)
+    state = {"scratch": None, "parts": None}
 
-    def barrier():
-        if dist:
-            tdist.barrier()
-
-    def step():
-        ptr, nb, _ = r.compress(d_in.data_ptr(), args.eb, mode)
-        r.decompress(ptr, nb, d_out.data_ptr())
+    def compress():
+        if not sharded:
+            ptr, nb, _ = r.compress(d_in.data_ptr(), args.eb, mode)
+            return ptr, nb
+        eb = args.eb
+        if mode == cz.Rel:  # r2r: eb times the whole field's value range (one all-reduce)
+            eb *= shard.global_value_ranges([r], [d_in], dist)[0]
+        r.compress_scan(d_in.data_ptr(), eb, hist.data_ptr())
+        shard.allreduce_histograms(hist, dist)  # RCCL, ordered on this stream: no host sync
+        ptr, nb, _ = r.compress_finish(hist.data_ptr())
         return ptr, nb
 
+    def step(acc=None):
+        t0 = time.perf_counter()
+        ptr, nb = compress()  # host-synchronous (the archive header is read back)
+        t1 = time.perf_counter()
+        if sharded:  # RCCL gather of the per-rank archives to the root
+            view, state["scratch"] = archive_view(ptr, nb, dev, state["scratch"])
+            state["parts"] = shard.gather_to_root(view, dist, 0)
+        t2 = time.perf_counter()
+        r.decompress(ptr, nb, d_out.data_ptr())
+        if acc is not None:
+            acc[0] += t1 - t0
+            acc[1] += t2 - t1
+        return ptr, nb
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    r.enable_timing(False)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -124,14 +261,15 @@ def main():
     assert err <= 1.001 * eb_abs + ulp, f"error bound violated: {err} > {eb_abs} (+ulp {ulp})"
 
     # timed region: the library's HIP-event stage timing is OFF (its event records would add
-    # barrier packets to the stream); the per-stage/kernel durations come from a second pass
-    r.enable_timing(False)
+    # barrier packets to the stream); the per-stage/kernel durations come from a second pass.
+    # Decompress is asynchronous: step i's decompress overlaps the host side of step i+1's
+    # compress on the same stream (nothing is skipped: every step's kernels run in order).
+    acc = [0.0, 0.0]
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        ptr, nb = step()
-        torch.cuda.synchronize()  # decompress is asynchronous; close the step
+        ptr, nb = step(acc)
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
@@ -142,17 +280,41 @@ def main():
         ptr, nb = step()
         torch.cuda.synchronize()
         stage_acc += np.array(r.stage_times())
-    if dist:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        dt = t.item()
+    r.enable_timing(False)
+    ptr, nb = step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        t = torch.tensor([dt, acc[0], acc[1], err / max(eb_abs, 1e-300)], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt, acc[0], acc[1], rel_err = t.tolist()
     ms_per_step = 1e3 * dt / args.steps
-    value = world * nbytes_in * args.steps / dt / 1e9
+    value = total_bytes * args.steps / dt / 1e9
     st = stage_acc / args.steps
     comp_ms, decomp_ms = st[cz.T_COMPRESS], st[cz.T_DECOMPRESS]
-    ratio = nbytes_in / nb
 
-    # dominant kernel roofline (algorithmic bytes per launch / event-measured duration)
+    # whole-field archive at the root: merge the gathered slabs (host), decompress it on the root
+    merged_ok, arch_bytes_total = None, nb
+    if sharded:
+        parts = state["parts"]
+        if rank == 0:
+            host_parts = [p.cpu().numpy().tobytes() for p in parts]
+            merged = shard.merge(host_parts, dims, [s.offset for s in shard.plan_slabs(dims, world)])
+            arch_bytes_total = len(merged)
+            hdr = cz.psz_header.from_buffer_copy(merged[:176])
+            r_full = cz.Resource(cz.F4 if esz == 4 else cz.F8, dims, predictor, stream=stream.cuda_stream,
+                                 header=hdr)
+            d_arch = torch.frombuffer(bytearray(merged), dtype=torch.uint8).to(dev)
+            out = torch.empty(n_full, dtype=tdt, device=dev)
+            r_full.decompress(d_arch.data_ptr(), len(merged), out.data_ptr())
+            torch.cuda.synchronize()
+            e_full = (out.double() - d_full.double()).abs().max().item()
+            merged_ok = bool(e_full <= 1.001 * eb_abs + ulp)
+            r_full.close()
+            del out, d_arch, d_full
+        barrier()
+    ratio = esz * n_full / arch_bytes_total if sharded else nbytes_in / nb
+
+    # dominant kernel roofline (algorithmic bytes per launch / event-measured duration), rank 0
     ino = r.internals()
     splen = r.header.splen
     arch_bytes = nb
@@ -184,10 +346,10 @@ def main():
     achieved = d_bytes / (d_ms * 1e-3) / 1e9 if d_ms > 0 else None
     # HBM bytes per launch of the same kernel from the committed PMC summary of THIS config
     # (profiles/pmc_config<N>.json: rocprofv3 FETCH_SIZE/WRITE_SIZE passes, scripts/pmc_config.sh);
-    # null when this config has not been profiled
+    # null when this config has not been profiled or the launch is a slab (N > 1)
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_config{args.config}.json")
-    if os.path.exists(pmc_path):
+    if os.path.exists(pmc_path) and not sharded:
         try:
             pmc = json.load(open(pmc_path))
             hits = [v["hbm_bytes_per_launch"] for k, v in pmc.items()
@@ -202,7 +364,7 @@ def main():
 
     # end-to-end path from/to host memory (pinned), for DESIGN.md (never `value`)
     e2e = None
-    if not args.no_e2e and not args.profile_only and rank == 0:
+    if not args.no_e2e and not args.profile_only and world == 1:
         h_in = d_in.cpu().pin_memory()
         h_arch = torch.empty(nb, dtype=torch.uint8).pin_memory()
         h_out = torch.empty(n, dtype=tdt).pin_memory()
@@ -221,11 +383,16 @@ def main():
         e2e = round(nbytes_in * reps / (time.perf_counter() - t1) / 1e9, 2)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_only and esz == 4 \
-            and predictor == cz.Lorenzo:
-        cpu = cpu_baseline(d_in, dims, args.eb, nbytes_in)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_only:
+        if predictor == cz.Spline:
+            cpu = {"value": None, "unit": "GB/s", "cores": 0, "kind": "reference",
+                   "reason": "the reference has no CPU spline path (spline3.inl is CUDA-only, SURVEY.md §0.5)"}
+        elif esz == 4:
+            cpu = cpu_baseline(d_in, dims, args.eb, nbytes_in)
 
     if rank == 0:
+        tg_ms = 1e3 * acc[1] / args.steps
+        tc_ms = 1e3 * acc[0] / args.steps
         line = {
             "metric": METRICS[args.config],
             # only config 2 is BASELINE.json's metric workload; the others use the same fields
@@ -236,19 +403,26 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if weak else "strong",
             "vs_baseline": None,
             "dtype": "f64" if esz == 8 else "f32",
-            "data": f"synthetic (SURVEY.md §8d config-{args.config} recipe, seed per rank)",
+            "data": f"synthetic (SURVEY.md §8d config-{args.config} recipe" + (", seed per rank)" if weak else ")"),
             "config": {"workload": f"config{args.config}: {dims[0]}x{dims[1]}x{dims[2]} "
                                    f"{'f64' if esz == 8 else 'f32'}, {'rel' if mode == cz.Rel else 'abs'} "
                                    f"eb={args.eb}, {'spline3' if predictor == cz.Spline else 'Lorenzo'} + "
                                    "histogram + Huffman, compress+decompress per step",
-                       "per_rank_field_bytes": nbytes_in, "parallelism": f"dp{world} (independent fields)"},
+                       "field_bytes": esz * n_full, "per_rank_bytes": nbytes_in,
+                       "parallelism": (f"dp{world} (tile-aligned z-slabs of one field: histogram all-reduce + "
+                                       "gather of the archives to rank 0)") if sharded else
+                                      (f"dp{world} (independent fields)" if weak else "single GPU")},
             "compress_gbps": round(nbytes_in / (comp_ms * 1e-3) / 1e9, 2) if comp_ms > 0 else None,
             "decompress_gbps": round(nbytes_in / (decomp_ms * 1e-3) / 1e9, 2) if decomp_ms > 0 else None,
             "compress_roofline_frac": round(nbytes_in / (comp_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if comp_ms > 0 else None,
             "decompress_roofline_frac": round(nbytes_in / (decomp_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if decomp_ms > 0 else None,
+            "phases_ms": {"compress": round(tc_ms, 4), "gather": round(tg_ms, 4),
+                          "decompress_and_rest": round(ms_per_step - tc_ms - tg_ms, 4)},
+            "field_compress_gbps": round(total_bytes / (tc_ms * 1e-3) / 1e9, 2) if tc_ms > 0 else None,
+            "field_compress_gather_gbps": round(total_bytes / ((tc_ms + tg_ms) * 1e-3) / 1e9, 2) if tc_ms > 0 else None,
             "compression_ratio": round(ratio, 3),
             "stages_ms": {k: round(float(st[i]), 4) for k, i in
                           [("predict", cz.T_PREDICT), ("book", cz.T_BOOK), ("encode", cz.T_ENCODE),
@@ -260,10 +434,11 @@ def main():
             "e2e_host_gbps": e2e,
             "max_abs_err": err,
         }
+        if sharded:
+            line["merged_archive_bytes"] = arch_bytes_total
+            line["merged_decompress_ok"] = merged_ok
         print(json.dumps(line), flush=True)
     r.close()
-    if dist:
-        tdist.destroy_process_group()
 
 
 def host_cpu_model():
@@ -282,9 +457,9 @@ def cpu_baseline(d_in, dims, eb, nbytes_in):
     travels to the GPU box with the tree) on the same field, this host:
       * 1 thread (the reference is single-threaded): c_lorenzo + histogram + codebook (compress;
         the reference has no CPU Huffman encoder) and x_lorenzo (decompress; no CPU decoder);
-      * all cores, parallelised by us: the same reference calls on z-slabs of 8-plane multiples
-        (tile-independent), one thread each (ctypes drops the GIL), wall time of the slowest +
-        one codebook.
+      * all cores, parallelised by us: the same reference calls on tile-aligned slabs (z: 8-plane,
+        2-D: 32-row, 1-D: 1024-element multiples; tile-independent), one thread each (ctypes
+        drops the GIL), wall time of the slowest + one codebook.
     Null if oracle/_ref is absent."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     try:
@@ -295,14 +470,16 @@ def cpu_baseline(d_in, dims, eb, nbytes_in):
         return None
     import concurrent.futures as cf
 
+    from cusz_amd.shard import plan_slabs, tile_extent
+
     host = d_in.cpu().numpy()
     aff = sorted(os.sched_getaffinity(0))
     t = pyoracle.ref_time_stages(host, dims, eb)
     total_ms = t["c_lorenzo"] + t["histogram"] + t["codebook"] + t["x_lorenzo"]
-    # all-core variant: z-slabs over min(cores, 16) threads (the GPU box grants 16 CPUs per GPU)
-    nth = max(1, min(len(aff), 16, dims[2] // 8))
-    from cusz_amd.shard import plan_slabs
-
+    # all-core variant: slabs along the slowest axis over min(cores, 16) threads (the GPU box
+    # grants 16 CPUs per GPU), at most one slab per tile row
+    axis, tl = tile_extent(dims)
+    nth = max(1, min(len(aff), 16, (dims[axis] + tl - 1) // tl))
     slabs = [sl for sl in plan_slabs(dims, nth) if sl.count]
     t0 = time.perf_counter()
     with cf.ThreadPoolExecutor(len(slabs)) as ex:
@@ -315,29 +492,20 @@ def cpu_baseline(d_in, dims, eb, nbytes_in):
                       f"codebook {t['codebook']:.2f} ms + x_lorenzo {t['x_lorenzo']:.0f} ms; "
                       "no CPU Huffman in the reference)",
             "all_cores": {"value": round(nbytes_in / (par_ms * 1e-3) / 1e9, 4), "cores": len(slabs),
-                          "kind": "reference, parallelised by us over z-slabs"}}
+                          "kind": "reference, parallelised by us over tile-aligned slabs"}}
 
 
 def bench_sharded(args, world, rank, dist, dev):
     """config 4: six Nyx-like 512^3 f32 fields, each split into tile-aligned z-slabs, slab r of
     every field on rank r.  One step = sharded compress of all six fields with one codebook per
-    field (pass 1 per slab, ONE all-reduce of the [6, 1024] histograms, finish per slab), then
-    the gather of every rank's six archives to rank 0.  value = 6 x 512 MiB / compress time
-    (max over ranks); the compress+gather time is reported beside it."""
-    import numpy as np
+    field (value ranges by the library's extrema kernel + one all-reduce, pass 1 per slab, ONE
+    all-reduce of the [6, 1024] histograms, finish per slab), then the gather of every rank's six
+    archives to rank 0.  value = 6 x 512 MiB / compress time (max over ranks); the
+    compress+gather time is reported beside it."""
     import torch
 
     import cusz_amd as cz
     from cusz_amd import datagen, shard
-
-    if dist is None or not world > 1:
-        import torch.distributed as tdist
-
-        if not tdist.is_initialized():
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ.setdefault("MASTER_PORT", str(29400 + os.getpid() % 1000))
-            tdist.init_process_group("nccl", rank=0, world_size=1)
-    import torch.distributed as tdist
 
     full = (512, 512, 512)
     # r2r 1e-4 (value-range relative): at abs 1e-4 (SURVEY.md §8d) the 200 G velocity fields put
@@ -348,43 +516,52 @@ def bench_sharded(args, world, rank, dist, dev):
     fields = datagen.nyx_fields_torch(full, device=dev, z0=z0, z1=z0 + sl.dims[2])
     stream = torch.cuda.current_stream(dev)
     res = [cz.Resource(cz.F4, sl.dims, stream=stream.cuda_stream) for _ in fields]
-    for r in res:
-        r.enable_timing(True)
+    hists = torch.empty((len(fields), 1024), dtype=torch.int32, device=dev)
     total_bytes = 6 * full[0] * full[1] * full[2] * 4
+    state = {"scratch": None}
 
     def compress():
-        return shard.compress_fields_sharded(res, fields, eb, tdist, mode=cz.Rel, device=dev)
+        return shard.compress_fields_sharded(res, fields, eb, dist, mode=cz.Rel, device=dev, hists=hists)
 
     def gather(arch):
         sizes = [nb for _, nb in arch]
-        buf = torch.empty(sum(sizes), dtype=torch.uint8, device=dev)
+        if state["scratch"] is None or state["scratch"].numel() < sum(sizes):
+            state["scratch"] = torch.empty(sum(sizes), dtype=torch.uint8, device=dev)
+        buf = state["scratch"][:sum(sizes)]
         off = 0
         for (p, nb) in arch:
             cz.hip_memcpy(buf.data_ptr() + off, p, nb, 3)
             off += nb
         meta = torch.tensor(sizes, dtype=torch.int64, device=dev)
-        return shard.gather_to_root(buf, tdist, 0), shard.gather_to_root(meta.view(torch.uint8), tdist, 0)
+        if dist is None:
+            return [buf], [meta.view(torch.uint8)]
+        return shard.gather_to_root(buf, dist, 0), shard.gather_to_root(meta.view(torch.uint8), dist, 0)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
 
     for _ in range(args.warmup):
         gather(compress())
     torch.cuda.synchronize(dev)
-    tdist.barrier()
+    barrier()
     tc = tg = 0.0
     for _ in range(args.steps):
-        torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        arch = compress()
-        torch.cuda.synchronize(dev)
+        arch = compress()  # host-synchronous (every slab's header is read back)
         t1 = time.perf_counter()
         got = gather(arch)
         torch.cuda.synchronize(dev)
         t2 = time.perf_counter()
         tc += t1 - t0
         tg += t2 - t1
-    tdist.barrier()
-    t = torch.tensor([tc, tc + tg], device=dev, dtype=torch.float64)
-    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-    tc, tcg = t.tolist()
+    barrier()
+    if dist is not None:
+        t = torch.tensor([tc, tc + tg], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        tc, tcg = t.tolist()
+    else:
+        tcg = tc + tg
     # validation on the root: merge the slabs of field 0 and decompress the merged archive
     merged_ok = None
     if rank == 0:
@@ -412,7 +589,7 @@ def bench_sharded(args, world, rank, dist, dev):
             "vs_baseline": None, "dtype": "f32", "data": "synthetic (SURVEY.md §8d config-4 recipe)",
             "config": {"workload": f"config4: 6 Nyx-like 512x512x512 f32 fields, r2r eb={eb}, z-slabs "
                                    f"{sl.dims[2]} planes per rank, global codebook per field",
-                       "parallelism": f"dp{world} (z-slabs, 1 all-reduce + gather to root)"},
+                       "parallelism": f"dp{world} (z-slabs, 2 all-reduces + gather to root)"},
             "compress_gather_ms_per_step": round(1e3 * tcg / args.steps, 4),
             "compress_gather_gbps": round(total_bytes * args.steps / tcg / 1e9, 2),
             "merged_field0_bytes": len(merged), "merged_field0_decompress_ok": merged_ok,
@@ -420,8 +597,7 @@ def bench_sharded(args, world, rank, dist, dev):
         print(json.dumps(line), flush=True)
     for r in res:
         r.close()
-    tdist.destroy_process_group()
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

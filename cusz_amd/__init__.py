@@ -100,7 +100,7 @@ EXPORTS = [
     "psz_amd_get_internals", "psz_amd_enable_timing", "psz_amd_stage_times", "psz_amd_set_sublen",
     "psz_amd_decode_codes", "psz_amd_set_decoder", "psz_amd_set_layout", "psz_amd_version",
     "psz_amd_compress_scan_float", "psz_amd_compress_scan_double", "psz_amd_compress_finish",
-    "psz_amd_merge_archives",
+    "psz_amd_merge_archives", "psz_amd_value_range",
 ]
 
 
@@ -149,6 +149,8 @@ def lib():
     L.psz_amd_compress_finish.restype = C.c_int
     L.psz_amd_compress_finish.argtypes = [P, P, C.POINTER(psz_header), C.POINTER(C.c_void_p),
                                           C.POINTER(C.c_size_t)]
+    L.psz_amd_value_range.restype = C.c_int
+    L.psz_amd_value_range.argtypes = [P, P, C.c_size_t, P]
     L.psz_amd_merge_archives.restype = C.c_int
     L.psz_amd_merge_archives.argtypes = [C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.c_int,
                                          C.POINTER(C.c_size_t), psz_len, P, C.c_size_t,
@@ -229,6 +231,12 @@ class Resource:
         if st != PSZ_SUCCESS:
             raise PszError(st, "psz_amd_compress_finish")
         return out.value, nbytes.value, st
+
+    def value_range(self, d_in: int, d_minmax: int, n: int = 0):
+        """{min, max} of a device field (doubles) -> d_minmax, on the manager's stream (no sync)."""
+        st = lib().psz_amd_value_range(self._h, C.c_void_p(d_in), n, C.c_void_p(d_minmax))
+        if st != PSZ_SUCCESS:
+            raise PszError(st, "psz_amd_value_range")
 
     def decompress(self, d_archive: int, nbytes: int, d_out: int):
         L = lib()

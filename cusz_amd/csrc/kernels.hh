@@ -171,7 +171,7 @@ struct SplineXArgs {
   const uint32_t* unsorted = nullptr; // device flag: use `bucket` instead of `cells`
   size_t nbucket = 0;
   // outlier index -> (x, y, z) by multiply-high: q = mulhi(i, m) >> s for divisors X and Y
-  // (set by the launcher; exact for i < 2^31, ndiv = false makes the kernel divide)
+  // (set by the launcher; exact for i < 2^31; ndiv = true makes the kernel divide instead)
   uint32_t mX = 0, sX = 0, mY = 0, sY = 0;
   bool ndiv = true;
 };

@@ -36,6 +36,45 @@ struct Part {
 
 size_t rvbk_bytes(int bklen) { return 4 * 64 + 2 * (size_t)bklen; }
 
+int ndim_of(psz_len l) { return l.z > 1 ? 3 : (l.y > 1 ? 2 : 1); }
+
+// A slab of the field: same extents on every axis but the split (slowest) one, and -- unless it
+// is the last slab -- a split extent that is a whole number of prediction tiles.
+bool slab_shape_ok(psz_len s, psz_len f, bool last)
+{
+  switch (ndim_of(f)) {
+    case 3: return s.x == f.x && s.y == f.y && s.z >= 1 && (last || s.z % 8 == 0);
+    case 2: return s.x == f.x && s.z == 1 && s.y >= 1 && (last || s.y % 32 == 0);
+    default: return s.y == 1 && s.z == 1 && s.x >= 1 && (last || s.x % 1024 == 0);
+  }
+}
+
+// phf sections of one part (hf_buf.cc:199-211): monotonic offsets inside the segment the psz
+// header gives the phf archive, tables sized by pardeg, bitstream by total_ncell, and every
+// chunk's cells inside the bitstream.
+bool phf_sections_ok(const Part& p, size_t seg)
+{
+  const uint32_t* pe = p.ph.entry;
+  const size_t pd = (size_t)(p.ph.pardeg > 0 ? p.ph.pardeg : 0);
+  if (p.ph.pardeg <= 0 || pe[PHFHEADER_END] > seg) return false;
+  for (int k = 1; k <= PHFHEADER_END; k++)
+    if (pe[k] < pe[k - 1]) return false;
+  if (pe[PHFHEADER_RVBK] < sizeof(phf_header) || pe[PHFHEADER_PAR_NBIT] - pe[PHFHEADER_RVBK] != rvbk_bytes(p.ph.bklen) ||
+      pe[PHFHEADER_PAR_ENTRY] - pe[PHFHEADER_PAR_NBIT] != 4 * pd ||
+      pe[PHFHEADER_BITSTREAM] - pe[PHFHEADER_PAR_ENTRY] != 4 * pd ||
+      pe[PHFHEADER_END] - pe[PHFHEADER_BITSTREAM] != 4 * p.ph.total_ncell)
+    return false;
+  const uint32_t* nb = reinterpret_cast<const uint32_t*>(p.phf + pe[PHFHEADER_PAR_NBIT]);
+  const uint32_t* en = reinterpret_cast<const uint32_t*>(p.phf + pe[PHFHEADER_PAR_ENTRY]);
+  for (size_t c = 0; c < pd; c++) {
+    uint32_t nbit, ent;
+    std::memcpy(&nbit, nb + c, 4);
+    std::memcpy(&ent, en + c, 4);
+    if ((uint64_t)ent + ((uint64_t)nbit + 31) / 32 > p.ph.total_ncell) return false;
+  }
+  return true;
+}
+
 }  // namespace
 
 extern "C" int psz_amd_merge_archives(const uint8_t* const* parts, const size_t* part_bytes, int nparts,
@@ -61,6 +100,9 @@ extern "C" int psz_amd_merge_archives(const uint8_t* const* parts, const size_t*
     p.phf = parts[i] + e[PSZHEADER_ENCODED];
     std::memcpy(&p.ph, p.phf, sizeof(phf_header));
     p.n = p.h.len.x * p.h.len.y * p.h.len.z;
+    // the part's own segments: outlier cells, phf sections inside the phf segment, chunk table
+    if ((size_t)e[PSZHEADER_ENC_PASS1_END] - e[PSZHEADER_SPFMT] != 8 * p.h.splen) return PSZ_ABORT_NOT_IMPLEMENTED;
+    if (!phf_sections_ok(p, e[PSZHEADER_SPFMT] - e[PSZHEADER_ENCODED])) return PSZ_ABORT_NOT_IMPLEMENTED;
     const Part& q = P[0];
     if (p.h.dtype != q.h.dtype || p.h.pipeline.predictor != q.h.pipeline.predictor || p.h.rc.radius != q.h.rc.radius ||
         p.h.rc.eb != q.h.rc.eb || p.ph.bklen != q.ph.bklen || p.ph.sublen != q.ph.sublen)
@@ -70,7 +112,11 @@ extern "C" int psz_amd_merge_archives(const uint8_t* const* parts, const size_t*
     if (std::memcmp(p.phf + PHFHEADER_FORCED_ALIGN, q.phf + PHFHEADER_FORCED_ALIGN, rv) != 0)
       return PSZ_ABORT_NOT_IMPLEMENTED;  // slabs were not compressed with one shared codebook
     // every slab but the last must end on a chunk boundary, or the merged chunking differs
-    if (i + 1 < nparts && p.n % (size_t)p.ph.sublen != 0) return PSZ_ABORT_NOT_IMPLEMENTED;
+    if (p.ph.sublen <= 0 || (i + 1 < nparts && p.n % (size_t)p.ph.sublen != 0)) return PSZ_ABORT_NOT_IMPLEMENTED;
+    // slabs split the slowest axis of the field: the faster extents must be the field's, and
+    // every slab but the last must end on a prediction-tile boundary (z: 8 planes, 2-D: 32 rows,
+    // 1-D: 1024 elements; launch.hh:47-121), or Lorenzo would cross the seam differently
+    if (!slab_shape_ok(p.h.len, full_len, i + 1 == nparts)) return PSZ_ABORT_UNSUPPORTED_DIMENSION;
     if (elem_offsets && elem_offsets[i] != n_total) return PSZ_ABORT_NOT_IMPLEMENTED;  // slabs in field order
     n_total += p.n;
     splen += p.h.splen;

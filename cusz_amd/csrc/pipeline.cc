@@ -498,10 +498,22 @@ struct Pipeline {
     const uint32_t eg = ++gate_epoch;
     const bool gated =
         can_wait_value && hipStreamWaitValue32(stream, (void*)flag(5), eg, hipStreamWaitValueGte) == hipSuccess;
+    // the gate must open on every path out of here, or the stream (and every later call on
+    // it) waits forever: an early error return before build_book() opens it in the destructor
+    struct GateGuard {
+      volatile uint32_t* f;
+      uint32_t e;
+      bool armed;
+      ~GateGuard()
+      {
+        if (armed) __atomic_store_n(f, e, __ATOMIC_RELEASE);
+      }
+    } guard{flag(5), eg, gated};
     auto build_book = [&]() -> int {
       int fs = wait_flag(2, eh);
       if (!fs) build_codebook(h_hist(), bklen, h_book(), h_revbook());
       if (gated) __atomic_store_n(flag(5), eg, __ATOMIC_RELEASE);  // always open the gate
+      guard.armed = false;
       return fs;
     };
     if (!gated)
@@ -609,6 +621,9 @@ struct Pipeline {
   template <typename T>
   int decompress(const psz_header* h, const uint8_t* in, T* out)
   {
+    // the decoders overwrite the code buffer a pending compress_finish would pack: a scan ->
+    // decompress -> finish sequence must fail cleanly instead of writing a corrupt archive
+    pend.active = false;
     const psz_predictor pred = h->pipeline.predictor;
     if (pred != Lorenzo && pred != LorenzoZigZag && pred != Spline) return PSZ_ABORT_NO_SUCH_PREDICTOR;
     const bool zz = pred == LorenzoZigZag;
@@ -655,7 +670,6 @@ struct Pipeline {
     uint32_t ahead = (uint32_t)(2.5 * words_per_sub) + 3;
     ahead = std::min(ahead, brick_decode_max_ahead());
     int waves = brick_decode_max_waves();
-    if (const char* w = getenv("CUSZ_AMD_DEC_WAVES")) waves = std::max(1, std::min(waves, atoi(w)));  // TEMP experiment
     while (waves > 1 && brick_decode_lds(waves) > 160 * 1024) waves--;
     // words from the bitstream start to the end of the archive (range of the decoder's loads)
     const size_t bits_off = phf_off + 128 + rvbk + 8 * (size_t)pd;
@@ -883,6 +897,21 @@ int psz_amd_compress_scan_double(psz_resource* m, psz_rc2 rc, double* in, uint32
 {
   const int s = scan_impl<double>(m, rc, in);
   return (s == PSZ_SUCCESS || s == PSZ_WARN_RADIUS_TOO_LARGE) ? export_hist(m, d_hist_out, s) : s;
+}
+
+int psz_amd_value_range(psz_resource* m, const void* in, size_t len, double* d_minmax)
+{
+  Pipeline* p = cusz_amd::P(m);
+  if (!p || !in || !d_minmax) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if (len == 0) len = p->n;
+  CUSZ_AMD_HIP_CHECK(hipSetDevice(p->device));
+  if (m->header->dtype == F4)
+    CUSZ_AMD_HIP_CHECK((hipError_t)cusz_amd::launch_extrema<float>(static_cast<const float*>(in), len, d_minmax,
+                                                                   p->ext_scratch(), p->stream));
+  else
+    CUSZ_AMD_HIP_CHECK((hipError_t)cusz_amd::launch_extrema<double>(static_cast<const double*>(in), len, d_minmax,
+                                                                    p->ext_scratch(), p->stream));
+  return PSZ_SUCCESS;
 }
 
 int psz_amd_compress_finish(psz_resource* m, const uint32_t* d_hist, psz_header* out_h, uint8_t** out,

@@ -93,44 +93,54 @@ def gather_to_root(buf, dist, root: int = 0):
 
 
 def allreduce_histograms(hists, dist):
-    """Sum the u32 histograms of every rank's slabs in one all-reduce.  `hists`: int64 tensor
-    [fields, bklen] (device for RCCL, host for gloo); summed in place and returned."""
+    """Sum the u32 histograms of every rank's slabs in one all-reduce.  `hists`: [fields, bklen]
+    integer tensor (int32 holding the u32 bit pattern on the device for RCCL, int64 on the host
+    for gloo); summed in place and returned."""
     dist.all_reduce(hists, op=dist.ReduceOp.SUM)
     return hists
 
 
-def global_value_ranges(fields, dist):
-    """Rel (r2r) mode across slabs: max - min of every field over all ranks (one all-reduce of
-    [fields, 2]; libcusz.cc:287-293 computes this range per field on one GPU)."""
+def global_value_ranges(resources, fields, dist):
+    """Rel (r2r) mode across slabs: max - min of every field over all ranks.  Each slab's range
+    comes from the library's extrema kernel (psz_amd_value_range: extrema.cuhip.inl:150-208, on
+    the manager's stream), then ONE all-reduce (MAX) of [fields, 2] = {-min, max}
+    (libcusz.cc:287-293 computes this range per field on one GPU)."""
     import torch
 
-    mm = torch.stack([torch.stack([-a.double(), b.double()]) for a, b in (torch.aminmax(f) for f in fields)])
-    dist.all_reduce(mm, op=dist.ReduceOp.MAX)
+    mm = torch.empty((len(fields), 2), dtype=torch.float64, device=fields[0].device)
+    for i, (r, f) in enumerate(zip(resources, fields)):
+        r.value_range(f.data_ptr(), mm[i].data_ptr(), f.numel())
+    mm[:, 0].neg_()
+    if dist is not None and dist.get_world_size() > 1:
+        dist.all_reduce(mm, op=dist.ReduceOp.MAX)
     return [float(hi + lo) for lo, hi in mm.tolist()]
 
 
-def compress_fields_sharded(resources, fields, eb, dist, mode=0, radius=512, device=None):
+def compress_fields_sharded(resources, fields, eb, dist, mode=0, radius=512, device=None, hists=None):
     """Sharded compress of several fields whose slabs (device tensors `fields`) this rank holds,
     with one codebook per field shared by all ranks: pass 1 per slab, ONE all-reduce of the
     [fields, bklen] histograms, then finish every slab.  Rel mode: eb times the field's global
     value range (one more all-reduce), the slabs then compress with that absolute bound.
+
+    The managers must run on the caller's current stream (torch.cuda.current_stream): RCCL
+    orders the all-reduce after the scans and the finish after the all-reduce on that stream,
+    so no host synchronisation is needed between the phases.  The u32 histogram sums are
+    reduced as int32 (the bit pattern is the u32 sum: every count is < 2^32).
     Returns [(archive_ptr, nbytes)] (device archives, valid until the manager's next compress)."""
     import torch
 
     bklen = 2 * radius
     f = len(resources)
-    ebs = [eb * r for r in global_value_ranges(fields, dist)] if mode == 1 else [eb] * f
-    h32 = torch.zeros((f, bklen), dtype=torch.int32, device=device)
+    ebs = [eb * r for r in global_value_ranges(resources, fields, dist)] if mode == 1 else [eb] * f
+    if hists is None:
+        hists = torch.empty((f, bklen), dtype=torch.int32, device=device)
     for i, (r, t) in enumerate(zip(resources, fields)):
-        r.compress_scan(t.data_ptr(), ebs[i], h32[i].data_ptr(), 0, radius)
-    torch.cuda.synchronize(device)  # the scans run on the managers' streams
-    h64 = h32.to(torch.int64)
-    allreduce_histograms(h64, dist)
-    g32 = h64.to(torch.int32).contiguous()  # u32 bit pattern (sums < 2^32)
-    torch.cuda.synchronize(device)  # g32 is read on the managers' streams
+        r.compress_scan(t.data_ptr(), ebs[i], hists[i].data_ptr(), 0, radius)
+    if dist is not None and dist.get_world_size() > 1:
+        allreduce_histograms(hists, dist)
     out = []
     for i, r in enumerate(resources):
-        ptr, nb, _ = r.compress_finish(g32[i].data_ptr())
+        ptr, nb, _ = r.compress_finish(hists[i].data_ptr())
         out.append((ptr, nb))
     return out
 
@@ -140,27 +150,6 @@ def merge(parts, full_dims, offsets=None) -> bytes:
     from . import merge_archives
 
     return merge_archives(parts, full_dims, offsets)
-
-
-def gather_bytes(buf, dist, root: int = 0):
-    """Gather variable-length uint8 tensors (one per rank) to every rank; returns the list on
-    `root` (None elsewhere).  Works for cuda tensors over RCCL and cpu tensors over gloo."""
-    import torch
-
-    world = dist.get_world_size()
-    n = torch.tensor([buf.numel()], dtype=torch.int64, device=buf.device)
-    sizes = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(sizes, n)
-    sizes = [int(s.item()) for s in sizes]
-    mx = max(sizes)
-    padded = torch.zeros(mx, dtype=torch.uint8, device=buf.device)
-    padded[: buf.numel()] = buf
-    out = torch.empty(world * mx, dtype=torch.uint8, device=buf.device)
-    dist.all_gather_into_tensor(out, padded) if hasattr(dist, "all_gather_into_tensor") and \
-        buf.device.type == "cuda" else dist.all_gather(list(out.view(world, mx).unbind(0)), padded)
-    if dist.get_rank() != root:
-        return None
-    return [out[r * mx: r * mx + sizes[r]] for r in range(world)]
 
 
 def archive_tensor(ptr: int, nbytes: int, device):

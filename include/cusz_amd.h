@@ -94,6 +94,13 @@ int psz_amd_compress_scan_double(psz_resource* m, psz_rc2 rc, double* IN_d_data,
 int psz_amd_compress_finish(psz_resource* m, const uint32_t* IN_d_hist, psz_header* OUT_header,
                             uint8_t** OUT_d_compressed, size_t* OUT_compressed_bytes);
 
+/* Value range of a device field of the manager's dtype and length: writes {min, max} as two
+ * doubles to OUT_d_minmax (device memory), queued on the manager's stream (no host sync).  The
+ * Rel (r2r) mode probe of libcusz.cc:287-293 / extrema.cuhip.inl:150-208, exported so that a
+ * sharded compress can all-reduce the slabs' ranges before pass 1.  IN_len = 0 means the
+ * manager's length. */
+int psz_amd_value_range(psz_resource* m, const void* IN_d_data, size_t IN_len, double* OUT_d_minmax);
+
 /* Merge per-slab archives (HOST memory, in field order) compressed with one shared codebook
  * into the archive of the whole field: the archive one process would have written for it
  * (chunks concatenated, par_entry rebased by the cells before each slab, outlier indices by

@@ -1,0 +1,76 @@
+"""Config 4 of BASELINE.json on one GPU: the six Nyx-like 512^3 f32 fields (datagen.nyx_fields_torch,
+SURVEY.md §8d), each split into the 8 tile-aligned z-slabs of an 8-GPU run, one manager per slab
+standing in for the ranks:
+  value range per slab (psz_amd_value_range) -> the all-reduce's arithmetic (MAX of {-min, max})
+  -> r2r 1e-4 bound; pass 1 per slab -> the histogram all-reduce's arithmetic (sum) -> finish per
+  slab with the shared codebook -> psz_amd_merge_archives.
+The merged archive must be byte-identical to one compress of the whole field, and decompress
+within the bound.  The Rel-mode whole-field compress must arrive at the same bound."""
+import numpy as np
+import pytest
+import torch
+
+import cusz_amd as cz
+from cusz_amd import datagen, shard
+from gpu_util import d2h, sync
+
+pytestmark = pytest.mark.gpu
+
+FULL = (512, 512, 512)
+WORLD = 8
+
+
+def test_nyx_six_fields_sharded_equals_whole():
+    slabs = shard.plan_slabs(FULL, WORLD)
+    assert [s.dims[2] for s in slabs] == [64] * WORLD
+    st = torch.cuda.current_stream().cuda_stream
+    res = [cz.Resource(cz.F4, s.dims, stream=st) for s in slabs]
+    whole = cz.Resource(cz.F4, FULL, stream=st)
+    out = torch.empty(FULL[0] * FULL[1] * FULL[2], dtype=torch.float32, device="cuda")
+    hists = torch.zeros((WORLD, 1024), dtype=torch.int32, device="cuda")
+    mm = torch.empty((WORLD, 2), dtype=torch.float64, device="cuda")
+    r2r = 1e-4
+    fields = datagen.nyx_fields_torch(FULL, device="cuda")
+    assert len(fields) == 6
+    for fi, f in enumerate(fields):
+        views = [f[s.offset:s.offset + s.count] for s in slabs]
+        for r, v, k in zip(res, views, range(WORLD)):
+            r.value_range(v.data_ptr(), mm[k].data_ptr(), v.numel())
+        sync()
+        lo, hi = mm[:, 0].min().item(), mm[:, 1].max().item()
+        assert lo == f.min().item() and hi == f.max().item()
+        eb = r2r * (hi - lo)
+        for k, (r, v) in enumerate(zip(res, views)):
+            r.compress_scan(v.data_ptr(), eb, hists[k].data_ptr())
+        sync()
+        g = hists.to(torch.int64).sum(0)
+        assert int(g.sum().item()) == f.numel()
+        g32 = g.to(torch.int32).contiguous()
+        parts = []
+        for r in res:
+            ptr, nb, _ = r.compress_finish(g32.data_ptr())
+            parts.append(d2h(ptr, nb).tobytes())
+        merged = shard.merge(parts, FULL, [s.offset for s in slabs])
+        ptr, nb, _ = whole.compress(f.data_ptr(), eb, cz.Abs)
+        single = d2h(ptr, nb).tobytes()
+        assert len(merged) == len(single), fi
+        assert merged == single, f"field {fi}: merged archive differs from the whole-field archive"
+        # Rel mode on the whole field finds the same absolute bound
+        whole.compress(f.data_ptr(), r2r, cz.Rel)
+        assert whole.header.rc.eb == eb
+        # the merged archive decompresses within the bound
+        d_arch = torch.frombuffer(bytearray(merged), dtype=torch.uint8).cuda()
+        hdr = cz.psz_header.from_buffer_copy(merged[:176])
+        rx = cz.Resource(cz.F4, FULL, stream=st, header=hdr)
+        out.fill_(float("nan"))
+        rx.decompress(d_arch.data_ptr(), len(merged), out.data_ptr())
+        sync()
+        err = (out.double() - f.double()).abs().max().item()
+        ulp = 2.0 ** -23 * max(abs(lo), abs(hi))
+        assert err <= 1.001 * eb + ulp, (fi, err, eb)
+        rx.close()
+        del d_arch
+        fields[fi] = None  # free the field before the next one
+    for r in res:
+        r.close()
+    whole.close()
