@@ -826,6 +826,10 @@ static int compress_impl(psz_resource* m, psz_rc2 rc, T* in, psz_header* out_h, 
   if (rc.radius > 512) rc.radius = 512, status = PSZ_WARN_RADIUS_TOO_LARGE;  // libcusz.cc:281-285
   m->header->rc = rc;
   m->header->user_input_eb = rc.eb;
+  // the value range is this call's (Rel mode) or none: the reference leaves the previous call's
+  // range in the header (libcusz.cc:287-293 writes it only in Rel mode), so an Abs archive's
+  // bytes would depend on the manager's history (per-call state reset)
+  m->header->min_val = m->header->max_val = 0;
   m->dict_size = (uint16_t)(rc.radius * 2);
   CUSZ_AMD_HIP_CHECK(hipSetDevice(p->device));  // the creation device (B.7; several GPUs per process)
   int s = p->compress<T>(m->header, in, out, outlen);
@@ -843,6 +847,7 @@ static int scan_impl(psz_resource* m, psz_rc2 rc, T* in)
   if (rc.radius > 512) rc.radius = 512, status = PSZ_WARN_RADIUS_TOO_LARGE;  // libcusz.cc:281-285
   m->header->rc = rc;
   m->header->user_input_eb = rc.eb;
+  m->header->min_val = m->header->max_val = 0;  // as compress_impl
   m->dict_size = (uint16_t)(rc.radius * 2);
   CUSZ_AMD_HIP_CHECK(hipSetDevice(p->device));
   const int s = p->compress_scan<T>(m->header, in);
