@@ -1,6 +1,6 @@
 // cusz_amd/csrc/brick.hip -- fused brick pipeline for gfx950: the Lorenzo predictor feeds the
-// Huffman packer directly (compress) and the Huffman decoder feeds the Lorenzo reconstructor
-// directly (decompress), so quant codes never touch HBM.
+// Huffman packer (compress) and the Huffman decoder feeds the Lorenzo reconstructor directly
+// (decompress).
 //
 // Reference semantics (unchanged, bit-exact): predictor lrz_c.cuhip.inl:275-372 (3D 8^3 tiles),
 // reconstruct lrz_x.cuhip.inl:271-360, histogram hist.cuhip.inl:55-89, chunked MSB-first
@@ -9,18 +9,20 @@
 // MI355X layout.  A wave owns a brick of W x 8 x 8 elements (W = 64 V: lane l holds x in
 // [l V, l V + V)).  The Huffman chunk length is W, so every brick ROW (fixed y, z) is exactly one
 // reference chunk: chunk c covers codes [c W, c W + W) of the linear (x-fastest) order.
-//   pass 1 (k_brick3_scan):  predict -> per-brick histogram (u16, kept for the reservation),
-//                            global histogram, outlier cells.  Reads the input once.
+//   pass 1 (k_brick3_scan):  predict -> codes in brick order (u16), per-unit histogram (u16,
+//                            kept for the plan), global histogram, outlier slots.  Reads the
+//                            input once.
 //   host:                    canonical codebook from the global histogram (exact reference heap).
-//   reserve (k_brick_reserve + k_brick_offsets): a brick's bits = sum(hist_b[s] * len[s]); its
-//                            region in the bitstream is that many bits plus one partial cell per
-//                            row -- an upper bound, known BEFORE encoding, so every brick writes
-//                            at a fixed offset: no look-back, no scratch, no gather.
-//   pass 2 (k_brick3_pack):  predict again -> codewords -> pack each row (= chunk) into LDS
-//                            cells -> store at region + running offset; par_nbit / par_entry.
-//   decompress (k_brick3_decode): stage the brick's 64 chunks into LDS with one coalesced
-//                            copy, decode one chunk per lane in x-blocks of 64 symbols into an
-//                            LDS code tile, reconstruct the block (reference scan order), store.
+//   plan (k_brick_plan):     a unit's bits = sum(hist_u[s] * len[s]); its region in the bitstream
+//                            is that many bits plus one partial cell per row -- an upper bound,
+//                            known BEFORE encoding, so every unit writes at a fixed offset: no
+//                            look-back, no scratch, no gather.  The last block writes the headers.
+//   pass 2 (k_brick3_pack):  codes (read back, not re-predicted) -> codewords -> pack each row
+//                            (= chunk) into LDS cells -> store at region + running offset;
+//                            par_nbit / par_entry; the unit's outlier slot is copied out.
+//   decompress (k_brick3_decode): one wave per brick, one chunk per lane decoded in x-blocks of
+//                            64 symbols into an LDS code tile; the block is reconstructed
+//                            (reference scan order) and stored as whole rows.
 // The archive is the reference phf format: par_entry[c] points at chunk c (the reference decoder
 // reads chunk c from there, hf_kernels.cuhip.inl:386-391); chunks are laid out brick by brick,
 // and the few cells between a brick's last chunk and the next region are zero.

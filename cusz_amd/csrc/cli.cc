@@ -73,6 +73,38 @@ static void quality(const T* a, const T* b, size_t n, double eb)
               maxe <= eb * 1.001 ? "bounded" : "NOT bounded", psnr, std::sqrt(mse) / rng);
 }
 
+// --dump hist,quant (compressor.inl:507-529): the histogram u32[2r] and the quant codes
+// u16[N] in index order, as <input>.<mode>_<eb>.bk_<2r>.{ht_u4,qt_u2}.  The codes are decoded
+// back from the archive with the per-chunk decoder (chunk c holds codes [c sublen, (c+1)
+// sublen) whatever the layout), so the dump is in index order for both layouts.
+static int dump_internals(const psz_ctx* ctx, psz_resource* m, uint8_t* d_arch, size_t n)
+{
+  const psz_header* h = ctx->header;
+  auto name = [&](const char* suffix, const char* t) {
+    return std::string(ctx->cli->file_input) + "." + ctx->cli->char_mode + "_" + ctx->cli->char_meta_eb + ".bk_" +
+           std::to_string(2 * h->rc.radius) + "." + suffix + "_" + t;
+  };
+  psz_amd_internals io;
+  if (psz_amd_get_internals(m, &io) != PSZ_SUCCESS) return 1;
+  if (ctx->cli->dump_hist) {
+    std::vector<uint32_t> hist((size_t)io.bklen);
+    CK(hipMemcpy(hist.data(), io.d_hist, hist.size() * 4, hipMemcpyDeviceToHost));
+    if (!write_file(name("ht", "u4"), hist.data(), hist.size() * 4)) return 1;
+  }
+  if (ctx->cli->dump_quantcode) {
+    std::printf("[psz::dump] dumping quantization codes to file: %s\n", name("qt", "u2").c_str());
+    if (psz_amd_set_decoder(m, PSZ_AMD_DECODER_LANE) != PSZ_SUCCESS || psz_amd_decode_codes(m, d_arch) != PSZ_SUCCESS) {
+      std::fprintf(stderr, "[cusz] cannot decode the archive for --dump quant\n");
+      return 1;
+    }
+    std::vector<uint16_t> q(n);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(q.data(), io.d_quant_codes, n * 2, hipMemcpyDeviceToHost));
+    if (!write_file(name("qt", "u2"), q.data(), n * 2)) return 1;
+  }
+  return 0;
+}
+
 int main(int argc, char** argv)
 {
   if (argc == 1) {
@@ -128,6 +160,7 @@ int main(int argc, char** argv)
     if (!ctx->cli->skip_tofile && !write_file(opath, arch.data(), bytes)) return 1;
     float ms[PSZ_AMD_T_COUNT];
     psz_amd_stage_times(m, ms, PSZ_AMD_T_COUNT);
+    if ((ctx->cli->dump_hist || ctx->cli->dump_quantcode) && dump_internals(ctx, m, d_arch, n)) return 1;
     std::printf("compressed %s -> %s: %zu -> %zu bytes, CR %.3f, outliers %zu\n", ctx->cli->file_input,
                 opath.c_str(), n * es, bytes, (double)(n * es) / bytes, (size_t)out_h.splen);
     if (ctx->cli->report_time)

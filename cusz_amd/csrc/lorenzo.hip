@@ -269,6 +269,10 @@ k_lorenzo_x1d(const uint16_t* __restrict__ codes, T* out, size_t n, T ebx2, T r,
     // just issued
     auto rlen = [&](size_t b0) { return (uint32_t)(n - b0 < 256 ? n - b0 : 256); };
     size_t cp = fused ? ox.bstart[brick] : 0;  // next cell of this brick
+    // one past the brick's last cell: a brick with fewer cells than zero codes (outliers dropped
+    // at the cap, always an index-order suffix) reads 0 for the missing ones, as the scatter
+    // path does, and never reaches into the next brick's cells
+    const size_t cend = fused ? ox.bstart[brick + 1] : 0;
     auto outliers = [&](const uint16_t (&c)[V], size_t b0, T (&o)[V]) {
       const uint32_t len = rlen(b0);
       if (!fused) {
@@ -291,7 +295,7 @@ k_lorenzo_x1d(const uint16_t* __restrict__ codes, T* out, size_t n, T ebx2, T r,
         T v = 0;
         if (z[k]) {
           const size_t j = cp + rank;
-          if (j < ox.ncell) v = (T)__builtin_bit_cast(float, ox.cells[2 * j]);
+          if (j < cend) v = (T)__builtin_bit_cast(float, ox.cells[2 * j]);
           rank++;
         }
         o[k] = v;

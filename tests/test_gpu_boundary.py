@@ -95,3 +95,22 @@ def test_decompress_rejects_truncated_archive():
     o = torch.empty(data.size, device="cuda")
     with pytest.raises(cz.PszError):
         r.decompress(ptr, nb - 8, o.data_ptr())  # in_len shorter than the header's entry[5]
+
+
+@pytest.mark.parametrize("dims", [(512, 24, 16), (300, 200, 1)])
+def test_cli_dump_hist_quant(oracle, tmp_path, dims):
+    """`--dump quant,hist` (compressor.inl:507-529): <input>.<mode>_<eb>.bk_<2r>.ht_u4 holds the
+    histogram and .qt_u2 the quant codes in index order (both layouts), equal to the oracle's."""
+    data = datagen.smooth3d_np(dims, 5) if dims[2] > 1 else datagen.cesm2d_np(dims[:2], 5)
+    f = tmp_path / "field.bin"
+    data.tofile(f)
+    lens = "x".join(str(d) for d in dims if d > 1)
+    z = subprocess.run([cz.CLI_PATH, "-z", "-t", "f32", "-m", "abs", "-e", "1e-4", "-l", lens, "-i", str(f),
+                        "--dump", "quant,hist"], capture_output=True, text=True, timeout=120)
+    assert z.returncode == 0, z.stderr
+    codes, _, _ = oracle.lorenzo_c(data, dims, 1e-4)
+    base = str(f) + ".abs_1e-4.bk_1024"
+    hist = np.fromfile(base + ".ht_u4", dtype=np.uint32)
+    np.testing.assert_array_equal(hist, oracle.histogram(codes))
+    q = np.fromfile(base + ".qt_u2", dtype=np.uint16)
+    np.testing.assert_array_equal(q, codes)

@@ -10,6 +10,7 @@ import torch.multiprocessing as mp
 
 from cusz_amd import datagen
 from cusz_amd.shard import plan_slabs
+from archive_util import oracle_archive
 
 
 @pytest.mark.parametrize("dims,world", [((64, 48, 40), 2), ((64, 48, 40), 3), ((64, 48, 41), 4),
@@ -47,36 +48,6 @@ def test_slab_codes_equal_full_field(oracle, dims, world):
 # Per-slab archives are built by the CPU oracle (no GPU here); the exchange (histogram
 # all-reduce, gather to root) and the merge are the product code (cusz_amd.shard,
 # psz_amd_merge_archives).
-def oracle_archive(oracle, codes, ol_val, ol_idx, dims, eb, book, rv, sublen, bklen=1024):
-    """Reference-layout archive (psz_header | phf segment | outlier cells) from oracle codes and
-    a given codebook (hf_buf.cc:191-211, compressor.inl:398-418)."""
-    import cusz_amd as cz
-
-    nbit, entry, bs, tot = oracle.hf_encode(codes, book, sublen)
-    pardeg = nbit.size
-    sizes = [oracle.PHF_FORCED_ALIGN, rv.size, 4 * pardeg, 4 * pardeg, 4 * bs.size]
-    ent = [0]
-    for s in sizes:
-        ent.append(ent[-1] + s)
-    phf = oracle.phf_header_bytes(bklen, sublen, pardeg, codes.size, tot, bs.size, ent)
-    phf += b"\0" * (oracle.PHF_FORCED_ALIGN - len(phf)) + rv.tobytes() + nbit.tobytes() + \
-        entry.tobytes() + bs.tobytes()
-    cells = np.empty((ol_idx.size, 2), np.uint32)
-    cells[:, 0] = np.asarray(ol_val, np.float32).view(np.uint32)
-    cells[:, 1] = ol_idx
-    h = cz.psz_header()
-    h.dtype, h.pipeline.predictor, h.pipeline.codec1 = cz.F4, cz.Lorenzo, cz.Huffman
-    h.rc.mode, h.rc.eb, h.rc.radius = cz.Abs, eb, bklen // 2
-    h.vle_sublen, h.vle_pardeg = sublen, pardeg
-    h.len.x, h.len.y, h.len.z = dims
-    h.splen = ol_idx.size
-    h.user_input_eb = eb
-    e = [0, 176, 176, 176 + len(phf), 176 + len(phf) + 8 * ol_idx.size, 176 + len(phf) + 8 * ol_idx.size]
-    for i, v in enumerate(e):
-        h.entry[i] = v
-    return bytes(h) + phf + cells.tobytes()
-
-
 def _sharded_worker(rank, world, port, dims, q):
     import sys
 
