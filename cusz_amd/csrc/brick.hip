@@ -658,7 +658,10 @@ __device__ __forceinline__ void recon_block(const uint16_t* tile, T* out, size_t
   const uint32_t voff = (uint32_t)lane * sizeof(T);
   const uint32_t l7 = (uint32_t)lane & 7u;
   T s[8];
-#pragma unroll
+#ifndef CUSZ_AMD_RECON_UNROLL
+#define CUSZ_AMD_RECON_UNROLL 8
+#endif
+#pragma unroll CUSZ_AMD_RECON_UNROLL
   for (int y = 0; y < 8; y++) {
     if ((uint32_t)y >= nyv) break;
     uint32_t cd[8];
@@ -674,13 +677,21 @@ __device__ __forceinline__ void recon_block(const uint16_t* tile, T* out, size_t
         v[z] = (T)cd[z] - r;
       anyz |= cd[z] == 0u;
     }
+#ifndef CUSZ_AMD_RECON_NOOL
     if (__builtin_amdgcn_ballot_w64(anyz)) {  // outliers: their values were scattered into out
+#else
+    if (false) {  // timing experiment: outliers not read
+#endif
+      // every row with an outlier is loaded whole (uniform branch), then one wait for all
+      T ov[8];
+#pragma unroll
+      for (int z = 0; z < 8; z++) {
+        ov[z] = T(0);
+        if (__builtin_amdgcn_ballot_w64(cd[z] == 0u) && (uint32_t)z < nzv) ov[z] = base[(size_t)z * plane + (size_t)y * lx + lane];
+      }
 #pragma unroll
       for (int z = 0; z < 8; z++)
-        if (cd[z] == 0u && (uint32_t)z < nzv) {
-          const T ov = base[(size_t)z * plane + (size_t)y * lx + lane];
-          v[z] = ZZ ? ov + T(0) : ov - r;
-        }
+        if (cd[z] == 0u) v[z] = ZZ ? ov[z] + T(0) : ov[z] - r;
     }
     T t[8];
 #pragma unroll
@@ -852,6 +863,209 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
 #endif
 }
 
+// =========================================================================================
+// decompress v2: register bit window, counted refills
+// =========================================================================================
+// Same work split as k_brick3_decode (one wave per brick, lane l decodes chunk l = brick row
+// (l / 8, l % 8) in blocks of 64 symbols, the block reconstructed with lane = column), but the
+// decode step keeps its bits in registers: w0:w1 is a 64-bit window (`sh` = 32 - bits consumed
+// of w0, so the next 32 chunk bits are alignbit(w0, w1, sh)), w2 and nx are the next two words.
+// A step is one table lookup (the only LDS round trip on the chain); when it crosses a word
+// boundary the words shift down and nx is refilled from the lane's LDS ring (word k in slot
+// k % kR2, [slot][lane]).  The ring is refilled every kF2 steps: each lane issues one 16-B load
+// of its next four words (or an out-of-range load that returns nothing) and writes the group it
+// loaded two refills earlier, so a load has 2 kF2 steps to land and the wait for it is a counted
+// vmcnt(1) -- never behind the reconstruction's stores, which are only issued after the ring
+// has been drained at the block's end.  A lane whose next word has not landed yet sits out
+// steps (its predicate is off) until it has; nothing ever waits in the step loop.
+#ifndef CUSZ_AMD_DEC2_F
+#define CUSZ_AMD_DEC2_F 8
+#endif
+#ifndef CUSZ_AMD_DEC2_WAVES
+#define CUSZ_AMD_DEC2_WAVES 8
+#endif
+constexpr int kF2 = CUSZ_AMD_DEC2_F;  // decode steps between ring refills
+constexpr uint32_t kR2 = 16;          // ring words per lane (power of two)
+constexpr size_t kDec2WaveBytes = (size_t)(kR2 + 1) * 64 * 4 + (size_t)64 * kTP * 2;  // ring + junk slot + tile
+constexpr int kDec2Waves = CUSZ_AMD_DEC2_WAVES;
+#ifndef CUSZ_AMD_DEC2_DBG
+#define CUSZ_AMD_DEC2_DBG 0
+#endif
+// timing experiments only (wrong output): 1 no reconstruction, 2 no tile stores, 4 L1 lookup
+// only, 8 every lane steps every step, 16 no ring reads
+constexpr int kDec2Dbg = CUSZ_AMD_DEC2_DBG;
+#ifndef CUSZ_AMD_DEC2_STEP_UNROLL
+#define CUSZ_AMD_DEC2_STEP_UNROLL 8
+#endif
+#ifndef CUSZ_AMD_DEC2_L2COND
+#define CUSZ_AMD_DEC2_L2COND 0
+#endif
+constexpr bool kDec2L2Cond = CUSZ_AMD_DEC2_L2COND;  // L2 table read only for the lanes L1 missed
+constexpr uint32_t kOOB = 0x80000000u;  // buffer offset past any bitstream: the load returns 0
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <typename T, bool ZZ, bool BUF>
+__global__ void __launch_bounds__(64 * kDec2Waves)
+k_brick3_decode2(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const uint8_t* __restrict__ revbook,
+                 int bklen, const uint32_t* __restrict__ par_nbit, const uint32_t* __restrict__ par_entry, T* out,
+                 uint32_t lx, uint32_t ly, uint32_t lz, T ebx2, T r, uint32_t nbx, uint32_t nby, uint32_t nbricks)
+{
+  __shared__ hfd::LdsTables<kDecB> tb;
+  extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
+  hfd::build_tables<kDecB>(tb, revbook, bklen);
+  const hfd::DecRegs rg = hfd::load_dec_regs(tb);
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t* ring_lane = reinterpret_cast<uint32_t*>(dsm + (size_t)wid * kDec2WaveBytes) + lane;
+  uint16_t* tile = reinterpret_cast<uint16_t*>(dsm + (size_t)wid * kDec2WaveBytes + (size_t)(kR2 + 1) * 64 * 4);
+  const __amdgpu_buffer_rsrc_t rbits =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(bitstream), 0, (int)(bs_words * 4u), (int)kBufRsrcW3);
+  const size_t plane = (size_t)lx * ly;
+  const uint32_t ubk = (uint32_t)bklen;
+  constexpr uint32_t W = 256;
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  const uint32_t ry = (uint32_t)lane >> 3, rz = (uint32_t)lane & 7u;
+
+  // diagnostic build (psz_amd_debug_brick_profile): 0 bricks, 1 brick-start cycles (loads and
+  // their wait), 2 decode-loop cycles, 3 drain cycles, 4 reconstruct cycles, 5 loop iterations,
+  // 6 lane-steps skipped for want of data, 7 lane-steps done
+  BPROF(unsigned long long pc[8] = {}; unsigned long long tk = __builtin_readcyclecounter(), tp = tk;)
+  for (uint32_t brick = blockIdx.x * (blockDim.x >> 6) + wid; brick < nbricks; brick += nw) {
+    BPROF(pc[0]++; tp = __builtin_readcyclecounter();)
+    const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
+    const uint32_t y0 = by * 8, z0 = bz * 8;
+    const bool live = y0 + ry < ly && z0 + rz < lz;
+    const size_t c = ((size_t)(z0 + rz) * ly + (y0 + ry)) * nbx + bx;
+    const uint32_t nbit = live ? par_nbit[c] : 0u;
+    const uint32_t vbase = (live ? par_entry[c] : 0u) * 4u;
+    const uint32_t nwords = (nbit + 31u) >> 5;
+    // words 0..7: 0..2 into registers, 3..7 into the ring
+    uint32_t w0 = 0, w1, w2, nx;
+    {
+      const u32x4 a0 = __builtin_amdgcn_raw_buffer_load_b128(rbits, (int)(live ? vbase : kOOB), 0, 0);
+      const u32x4 a1 = __builtin_amdgcn_raw_buffer_load_b128(rbits, (int)(live ? vbase + 16u : kOOB), 0, 0);
+      w1 = a0.x, w2 = a0.y, nx = a0.z;
+      ring_lane[3 * 64] = a0.w;
+      ring_lane[4 * 64] = a1.x, ring_lane[5 * 64] = a1.y, ring_lane[6 * 64] = a1.z, ring_lane[7 * 64] = a1.w;
+    }
+    uint32_t kk = 2;           // word index held by nx
+    uint32_t ctop = 8;         // words [0, ctop) have been written (ring or registers)
+    uint32_t ltop = 8;         // words [0, ltop) have been requested
+    uint32_t sh = 0;           // 32 - bits of w0 consumed
+    uint32_t cnt = live ? 0u : 0x40000000u;  // a dead lane never steps
+    uint32_t keep = 0;         // symbol at the even column before an odd cnt (see the tile stores)
+    uint32_t rdy = ctop >= nwords ? 0xFFFFFFFFu : ctop;  // the lane steps while kk + 1 < rdy
+    u32x4 pa, pb;              // groups in flight (loaded one / two refills ago)
+    bool fa = false, fb = false;
+
+    BPROF(hfd::wave_sync(); tk = __builtin_readcyclecounter(); pc[1] += tk - tp; tp = tk;)
+    auto issue = [&](u32x4& p, bool& f) {
+      const bool ok = ltop < nwords && ltop + 4u <= kk + kR2;
+      p = __builtin_amdgcn_raw_buffer_load_b128(rbits, (int)(ok ? vbase + ltop * 4u : kOOB), 0, 0);
+      f = ok;
+      ltop += ok ? 4u : 0u;
+    };
+    // Write a landed group into the ring.  The stores are unconditional (a lane without a group
+    // writes the junk slot kR2), so the compiler's wait for the load sits here on every path and
+    // no load is left pending past the block's end.
+    auto consume = [&](const u32x4& p, bool& f) {
+      const uint32_t s0 = f ? ctop : kR2 * 4u;  // kR2 * 4: every word goes to slot kR2
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t slot = f ? ((s0 + (uint32_t)i) & (kR2 - 1u)) : kR2;
+        ring_lane[slot * 64] = p[i];
+      }
+      ctop += f ? 4u : 0u;
+      f = false;
+      rdy = ctop >= nwords ? 0xFFFFFFFFu : ctop;
+    };
+
+    for (int blk = 0; blk < (int)(W / kBlk); blk++) {
+      uint16_t* rowp = tile + lane * kTP - blk * kBlk;  // rowp[cnt] = tile column cnt - 64 blk
+      const uint32_t target = (uint32_t)(blk + 1) * kBlk;
+      auto steps = [&]() {
+#pragma unroll CUSZ_AMD_DEC2_STEP_UNROLL
+        for (int st = 0; st < kF2; st++) {
+          BPROF(pc[6] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(cnt < target && !(kk + 1u < rdy)));
+                pc[7] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(cnt < target && kk + 1u < rdy));)
+          if ((kDec2Dbg & 8) || (cnt < target && kk + 1u < rdy)) {
+            const uint32_t win = __builtin_amdgcn_alignbit(w0, w1, sh);  // chunk bits [pos, pos + 32)
+            uint32_t e;
+            if constexpr (kDec2Dbg & 4)
+              e = tb.l1[win >> (32 - kDecB)] | 0x04000000u;
+            else if constexpr (kDec2L2Cond)
+              e = hfd::lookup_l1_first<kDecB>(tb, rg, win, ubk);
+            else
+              e = hfd::lookup<kDecB>(tb, rg, win, ubk);
+            // symbols go to the tile as aligned u32 pairs: at an even column the entry's two
+            // symbols (the second is overwritten next step unless the entry holds two); at an odd
+            // column the symbol kept from the previous step and this step's first.  `keep` then
+            // holds the symbol the next odd-column store needs.
+            {
+              const uint32_t sy = e & hfd::kEntSymMask;
+              const bool odd = cnt & 1u;
+              const uint32_t word = odd ? (keep | (sy << 16)) : sy;
+              if constexpr (!(kDec2Dbg & 2)) *reinterpret_cast<uint32_t*>(rowp + (cnt & ~1u)) = word;
+              keep = odd ? (sy >> 16) : (sy & 0xFFFFu);
+            }
+            cnt += hfd::ent_nsym(e);
+            const int32_t s2 = (int32_t)sh - (int32_t)hfd::ent_bits(e);
+            const bool shf = s2 < 0;
+            sh = (uint32_t)s2 & 31u;
+            if constexpr (kDec2Dbg & 64) {  // branch-free shift, nx re-read every step
+              w0 = shf ? w1 : w0;
+              w1 = shf ? w2 : w1;
+              w2 = shf ? nx : w2;
+              kk += shf ? 1u : 0u;
+              nx = ring_lane[(kk & (kR2 - 1u)) * 64];
+            }
+            else if (shf) {  // crossed into the next word: shift, refill nx from the ring
+              w0 = w1, w1 = w2, w2 = nx;
+              kk++;
+              if constexpr (kDec2Dbg & 16)
+                nx = nx * 0x9E3779B9u + kk;
+              else
+                nx = ring_lane[(kk & (kR2 - 1u)) * 64];
+            }
+          }
+        }
+      };
+      // a group is written into the ring two refills after its load; the first wait of a block
+      // comes 2 kF2 steps after the previous block's stores
+      issue(pa, fa);
+      steps();
+      issue(pb, fb);
+      steps();
+      do {
+        consume(pa, fa);
+        issue(pa, fa);
+        steps();
+        consume(pb, fb);
+        issue(pb, fb);
+        steps();
+        BPROF(pc[5]++;)
+      } while (__builtin_amdgcn_ballot_w64(cnt < target));
+      BPROF(hfd::wave_sync(); tk = __builtin_readcyclecounter(); pc[2] += tk - tp; tp = tk;)
+      consume(pa, fa);  // drain: nothing stays in flight across the stores below
+      consume(pb, fb);
+      hfd::wave_sync();
+      BPROF(tk = __builtin_readcyclecounter(); pc[3] += tk - tp; tp = tk;)
+      {
+        const uint32_t nyv = min(8u, ly - y0), nzv = min(8u, lz - z0);
+        const size_t base_elem = (size_t)z0 * plane + (size_t)y0 * lx + (size_t)bx * W + (size_t)blk * kBlk;
+        if constexpr (!(kDec2Dbg & 1)) recon_block<T, ZZ, BUF>(tile, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane);
+      }
+      hfd::wave_sync();
+      BPROF(tk = __builtin_readcyclecounter(); pc[4] += tk - tp; tp = tk;)
+      // (a two-symbol step that crossed the block end keeps the next block's first symbol in
+      // `keep`: cnt is odd, so the next block's first store writes it to column 0)
+    }
+  }
+#ifdef CUSZ_AMD_DEC_PROFILE
+  if (lane == 0)
+    for (int i = 0; i < 8; i++) atomicAdd(&g_brick_prof[i], pc[i]);
+#endif
+}
+
 }  // namespace
 
 // =========================================================================================
@@ -964,14 +1178,30 @@ int launch_brick_decode(const BrickLaunch& L, const uint32_t* bitstream, size_t 
   const T ebx2 = (T)(eb * 2);  // lrz_x.cuhip.inl:432
   const T r = (T)radius;
   const BrickGeom& g = L.g;
-  if (brick_decode_lds(waves) > 160 * 1024 || waves < 1 || waves > kDecMaxWaves || bs_words >= (1ull << 30))
-    return (int)hipErrorInvalidValue;
-  const size_t lds = (size_t)waves * kDecWaveBytes;  // dynamic part
+  if (bs_words >= (1ull << 30)) return (int)hipErrorInvalidValue;
   const int grid = L.ncu;
   // buffer stores address a brick block with 32-bit offsets from its first element
   const size_t plane = (size_t)L.lx * L.ly;
   const bool buf = (7 * plane + 7 * (size_t)L.lx + (size_t)kBlk) * sizeof(T) < (1ull << 31);
   const uint32_t bw = (uint32_t)bs_words;
+  static const bool v1 = getenv("CUSZ_AMD_BRICK_DEC_V1") != nullptr;  // TEMP: A/B of the two decoders
+  if (!v1) {
+    const size_t lds = (size_t)kDec2Waves * kDec2WaveBytes;
+#define DEC2_LAUNCH(ZZ, BUF)                                                                                        \
+  k_brick3_decode2<T, ZZ, BUF><<<grid, 64 * kDec2Waves, lds, st>>>(bitstream, bw, revbook, bklen, par_nbit, par_entry, \
+                                                                   out, L.lx, L.ly, L.lz, ebx2, r, g.nbx, g.nby,      \
+                                                                   g.nbricks)
+    if (zz) {
+      if (buf) DEC2_LAUNCH(true, true); else DEC2_LAUNCH(true, false);
+    }
+    else {
+      if (buf) DEC2_LAUNCH(false, true); else DEC2_LAUNCH(false, false);
+    }
+#undef DEC2_LAUNCH
+    return (int)hipGetLastError();
+  }
+  if (brick_decode_lds(waves) > 160 * 1024 || waves < 1 || waves > kDecMaxWaves) return (int)hipErrorInvalidValue;
+  const size_t lds = (size_t)waves * kDecWaveBytes;  // dynamic part
 #define DEC_LAUNCH(ZZ, BUF)                                                                                       \
   k_brick3_decode<T, ZZ, BUF><<<grid, 64 * waves, lds, st>>>(bitstream, bw, revbook, bklen, par_nbit, par_entry, out, \
                                                              L.lx, L.ly, L.lz, ebx2, r, g.nbx, g.nby, g.nbricks,      \

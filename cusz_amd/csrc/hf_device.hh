@@ -137,6 +137,9 @@ __device__ __forceinline__ uint32_t tab_decode1(uint32_t v, const uint32_t* firs
 //  Codes longer than 16 bits (or past the cap) count failing lengths against thresholds the
 //  caller keeps in registers (DecRegs).
 constexpr int kL2Bits = 16;
+#ifndef CUSZ_AMD_SLOW_UNROLL
+#define CUSZ_AMD_SLOW_UNROLL 16  // unroll of the rare >16-bit code search (1: keep it small)
+#endif
 #ifndef CUSZ_AMD_DEC_L2CAP
 #define CUSZ_AMD_DEC_L2CAP 4096
 #endif
@@ -227,12 +230,34 @@ __device__ __forceinline__ uint32_t lookup(const LdsTables<B>& t, const DecRegs&
   uint32_t e = e1 | e2;
   if (__builtin_expect(e == 0, 0)) {  // all lengths <= 16 failed: count the rest
     uint32_t l = B + 1;
-#pragma unroll
+#pragma unroll CUSZ_AMD_SLOW_UNROLL
     for (int q = B + 1 - kSlowFrom; q < kLmax - kSlowFrom + 1; q++)
       l += (kSlowFrom + q < (int)rg.maxl && (win >> (32 - (kSlowFrom + q))) < rg.first[q]) ? 1u : 0u;
     if (l > rg.maxl) l = rg.maxl;
     const uint32_t s = t.keys[min(t.base[l] + (win >> (32 - l)), bklen - 1)];
     e = ent_pack(0, l, s, 0);
+  }
+  return e;
+}
+
+// Same entry as lookup(), reading the L2 table only for the lanes whose L1 entry is 0 (a second,
+// dependent LDS round trip for them instead of an L2 read by every lane on every step).
+template <int B>
+__device__ __forceinline__ uint32_t lookup_l1_first(const LdsTables<B>& t, const DecRegs& rg, uint32_t win,
+                                                    uint32_t bklen)
+{
+  uint32_t e = t.l1[win >> (32 - B)];
+  if (e == 0) {
+    e = t.l2[min(win >> (32 - kL2Bits), (uint32_t)kL2Cap - 1)];
+    if (__builtin_expect(e == 0, 0)) {
+      uint32_t l = B + 1;
+#pragma unroll CUSZ_AMD_SLOW_UNROLL
+      for (int q = B + 1 - kSlowFrom; q < kLmax - kSlowFrom + 1; q++)
+        l += (kSlowFrom + q < (int)rg.maxl && (win >> (32 - (kSlowFrom + q))) < rg.first[q]) ? 1u : 0u;
+      if (l > rg.maxl) l = rg.maxl;
+      const uint32_t s = t.keys[min(t.base[l] + (win >> (32 - l)), bklen - 1)];
+      e = ent_pack(0, l, s, 0);
+    }
   }
   return e;
 }

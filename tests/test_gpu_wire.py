@@ -48,7 +48,8 @@ def test_decompress_oracle_archive(oracle, name, sublen):
     sync()
     got = d2h(out.data_ptr(), 4 * want.size, np.float32)
     np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
-    assert np.abs(got.astype(np.float64) - data).max() <= 1.001 * EB
+    ulp = 2.0 ** -23 * float(np.abs(data).max())  # f32 rounding of the reconstruction
+    assert np.abs(got.astype(np.float64) - data).max() <= 1.001 * EB + ulp
 
 
 @pytest.mark.parametrize("name,sublen", [("1d", 2048), ("2d", 4864), ("3d", 256), ("3d_brickwidth", 256)])
