@@ -26,6 +26,8 @@
 // The archive is the reference phf format: par_entry[c] points at chunk c (the reference decoder
 // reads chunk c from there, hf_kernels.cuhip.inl:386-391); chunks are laid out brick by brick,
 // and the few cells between a brick's last chunk and the next region are zero.
+#include <algorithm>
+
 #include "archive_device.hh"
 #include "common.hh"
 #include "hf_device.hh"
@@ -49,7 +51,6 @@ constexpr int kUnitBricks = 1;
 constexpr int kHistCopies = CUSZ_AMD_HIST_COPIES;  // lane-interleaved copies of a wave's brick histogram
 // per-brick u16 histograms are stored at a stride of whole 16-B groups (the plan kernel's loads)
 __host__ __device__ constexpr int bhist_stride(int bklen) { return (bklen + 7) & ~7; }
-constexpr int kWorkShards = 8;  // decoder work counters, 64 B apart
 
 __device__ __forceinline__ uint32_t readlane(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
 
@@ -260,9 +261,13 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
             bool is_ol;
             qc[k] = quantize<T, ZZ>(d[k], r, is_ol, olv[k]);
             anyol |= __ballot(is_ol);
+#ifndef CUSZ_AMD_SCAN_NOHIST  // (timing experiment switch: no histogram)
             atomicAdd(&s_hist[qc[k] * kHistCopies + hc], 1u);
+#endif
           }
+#ifndef CUSZ_AMD_SCAN_NOCODES  // (timing experiment switch: no code stores)
           store_codes_row<V>(cbrick + (size_t)row * (64 * V), qc);
+#endif
           if (anyol) {
             uint32_t mask = 0;
             size_t idx[V];
@@ -530,44 +535,61 @@ k_brick3_pack(const uint16_t* __restrict__ bcodes, uint32_t ly, uint32_t lz, con
 // =========================================================================================
 // decompress: chunk decode + reconstruct, one wave per brick
 // =========================================================================================
-// Lane l decodes chunk l of the brick (brick row (y, z) = (l / 8, l % 8)), 32 symbols per
-// sub-block, into an LDS code tile [row][column]; every 64 columns the wave reconstructs the
-// block with lane = column (y running sums and z Hillis-Steele in registers, x Hillis-Steele
-// across lanes by DPP) and stores whole 256-B rows.
+// Lane l decodes chunk l of the brick (brick row (y, z) = (l / 8, l % 8)) in blocks of 64
+// symbols into an LDS code tile [row][column]; after each block the wave reconstructs it with
+// lane = column (y running sums and z Hillis-Steele in registers, x Hillis-Steele across lanes by
+// DPP) and stores whole 256-B rows.
 //
-// Input ring.  Row k of a wave's ring holds word k of all 64 chunks ([word][lane]: a lane's
-// reads never conflict), rows in descending slots with a copy of row 0 below the first slot,
-// so that the pair (k, k + 1) is always one ds_read2 that lands as the 64-bit value {k : k+1}.  Rows are loaded by buffer loads (range-checked against the
-// bitstream, per-lane chunk offset in the VGPR offset, row in the SGPR offset) one sub-block
-// ahead and written to the ring at the next sub-block; a lane that outruns the resident rows
-// reads HBM.  The decode step keeps only a bit position: peek 32 bits at `pos` from the word
-// pair, look up one or two codes, store them, advance.
+// Decode step.  The lane keeps its bits in registers: w0:w1 is a 64-bit window (`sh` = 32 - bits
+// of w0 consumed, so the next 32 chunk bits are alignbit(w0, w1, sh)), w2 and nx are the next two
+// words.  A step is one table lookup (L1: one or two codes of <= 12 bits; L2: one code of <= 16
+// bits, read together; longer codes by threshold counting, hf_device.hh), the symbols' store to
+// the tile, and, when the step crosses a word boundary, a shift of the window with nx refilled
+// from the lane's LDS ring (word k in slot k % kRing, [slot][lane]: conflict-free).
+//
+// Ring refills are wave-uniform, every kF steps: each lane issues one 16-B load of its next four
+// words (or an out-of-range load that returns nothing, when its ring is full or its chunk read)
+// and writes the group it loaded two refills earlier, so a load has 2 kF steps to land and the
+// wait for it is a counted vmcnt(1) -- never behind the reconstruction's stores, which are only
+// issued after the ring has been drained at the block's end.
+//
+// Steps are grouped in quarters of kF: a lane takes part in a whole quarter or sits it out,
+// decided once from its column count and ring fill (one word crossed per step at most), so the
+// steps carry no predicates.  A lane may thus run up to 2 kF - 1 symbols past the block end,
+// into tile columns [64, 64 + 2 kF], which move to the block's front after the reconstruction.
+// Tile stores are aligned 32-bit pairs (a 2-B aligned 32-bit LDS store stalls the LDS pipeline,
+// SQ_LDS_UNALIGNED_STALL): at an even column the entry's two symbols, at an odd column the symbol
+// kept from the previous step and this step's first.
+//
+// Outliers.  When the archive's cells are grouped by brick and sorted by (row, x) -- this
+// compressor writes them so, k_brick_cell_bounds checks -- the k-th zero code of a row takes the
+// row's k-th cell (values staged in LDS per brick), and no scatter pass runs; otherwise the
+// scatter pass has written the values into `out`, where the reconstruction reads them.
 #ifndef CUSZ_AMD_DEC_B  // tuning knobs (overridable at build time for experiments)
 #define CUSZ_AMD_DEC_B 12
 #endif
-#ifndef CUSZ_AMD_DEC_RING
-#define CUSZ_AMD_DEC_RING 16
+#ifndef CUSZ_AMD_DEC_F
+#define CUSZ_AMD_DEC_F 4
 #endif
-#ifndef CUSZ_AMD_DEC_PF
-#define CUSZ_AMD_DEC_PF 8
+#ifndef CUSZ_AMD_DEC_WAVES
+#define CUSZ_AMD_DEC_WAVES 8
 #endif
-#ifndef CUSZ_AMD_DEC_STEPS
-#define CUSZ_AMD_DEC_STEPS 4
-#endif
-#ifndef CUSZ_AMD_DEC_REFILL
-#define CUSZ_AMD_DEC_REFILL 4
-#endif
-constexpr int kDecB = CUSZ_AMD_DEC_B;            // L1 decode table index bits
-constexpr int kSteps = CUSZ_AMD_DEC_STEPS;       // decode steps per loop iteration
-constexpr int kRefillEvery = CUSZ_AMD_DEC_REFILL;  // loop iterations between ring refills (power of 2)
-constexpr int kBlk = 64;                         // columns reconstructed per block (= lanes)
-constexpr int kTP = kBlk + 2;                    // tile row pitch (u16): row r starts at bank r
-constexpr uint32_t kRing = CUSZ_AMD_DEC_RING;    // ring rows (chunk words per lane), power of two
-constexpr int kPF = CUSZ_AMD_DEC_PF;             // ring rows loaded per sub-block at most
-constexpr uint32_t kRingWords = (kRing + 1) * 64;
-constexpr size_t kDecWaveBytes = kRingWords * 4 + (size_t)64 * kTP * 2;
-constexpr int kDecMaxWaves = 12;
-constexpr uint32_t kBufRsrcW3 = 0x00020000;     // raw buffer resource word 3 (gfx9)
+constexpr int kDecB = CUSZ_AMD_DEC_B;        // L1 decode table index bits
+constexpr int kF = CUSZ_AMD_DEC_F;           // decode steps between ring refills
+constexpr int kDecWaves = CUSZ_AMD_DEC_WAVES;  // waves per workgroup (one workgroup per CU)
+constexpr int kBlk = 64;                     // columns reconstructed per block (= lanes)
+constexpr uint32_t kRing = 16;               // ring words per lane (power of two)
+constexpr int kTP = kBlk + 2 + 2 * kF;       // tile row pitch (u16), an odd number of dwords
+static_assert(((kTP / 2) & 1) == 1, "odd dword pitch: row r starts at bank (kTP / 2) r");
+constexpr uint32_t kCellCap = 128;           // outlier values of a brick kept in LDS
+// per wave: ring + junk slot | tile | cell values | row starts (65) | row carries (64)
+constexpr size_t kDecTile = (size_t)(kRing + 1) * 64 * 4;
+constexpr size_t kDecCells = kDecTile + (size_t)64 * kTP * 2;
+constexpr size_t kDecRows = kDecCells + (size_t)kCellCap * 4;
+constexpr size_t kDecWaveBytes = kDecRows + (size_t)(65 + 64) * 4;
+constexpr uint32_t kBufRsrcW3 = 0x00020000;  // raw buffer resource word 3 (gfx9)
+constexpr uint32_t kOOB = 0x80000000u;       // buffer offset past any bitstream: the load returns 0
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint32_t wave_min(uint32_t v)
 {
@@ -586,19 +608,6 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v)
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d));
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-}
-
-// Chunk words k, k + 1 from HBM for a lane past the resident ring rows (rare).  The loads and
-// their wait are inline asm: a compiler-visible load here would make the waitcnt pass place a
-// vmcnt(0) -- which also waits for every in-flight ring load and output store -- at the join.
-__device__ __forceinline__ void fallback_pair(const uint32_t* g, uint32_t k, uint32_t lim, uint32_t& w0, uint32_t& w1)
-{
-  const uint32_t* p0 = g + (k < lim ? k : lim - 1u);
-  const uint32_t* p1 = g + (k + 1u < lim ? k + 1u : lim - 1u);
-  asm volatile("global_load_dword %0, %2, off\n\tglobal_load_dword %1, %3, off\n\ts_waitcnt vmcnt(0)"
-               : "=&v"(w0), "=&v"(w1)
-               : "v"(p0), "v"(p1)
-               : "memory");
 }
 
 // x Hillis-Steele inside 8-wide tiles across lanes (lrz_x.cuhip.inl:311-353 order: d = 1, 2, 4;
@@ -646,27 +655,39 @@ __device__ __forceinline__ void buf_store<double>(double v, __amdgpu_buffer_rsrc
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, (int)voff, (int)soff, 0);
 }
 
-// Reconstruct columns [xg0, xg0 + 64) of the brick from the code tile (lane = column).
-// lrz_x.cuhip.inl:271-360 order: v = (outlier + code) - r; y running sum (sequential); x then z
-// Hillis-Steele; times 2 eb.  `out` holds the scattered outlier values (read where code == 0).
-template <typename T, bool ZZ, bool BUF>
+// Outlier values of one brick for the reconstruction, without the scatter pass: the archive's
+// cells of the brick are contiguous and sorted by (row, x) (this compressor writes them so; a
+// bounds pass checks it), so the k-th zero code of a row, in x order, takes the row's k-th cell.
+// `val` holds the brick's values in LDS (or points at the archive's cells, stride 2 words, when
+// the brick has more than fit), row_start[64 + 1] the first cell of each row, carry[64] the cells
+// of each row consumed by earlier blocks.
+struct BrickCells {
+  const uint32_t* val;   // value bits of cell j at val[j * vstride]
+  uint32_t vstride;
+  uint32_t* row_start;   // LDS, 65 entries
+  uint32_t* carry;       // LDS, 64 entries
+};
+
+// Reconstruct columns [xg0, xg0 + 64) of the brick from the code tile (lane = column, row pitch
+// TP).  lrz_x.cuhip.inl:271-360 order: v = (outlier + code) - r; y running sum (sequential); x then
+// z Hillis-Steele; times 2 eb.  Outlier values (code 0) come from the ranked cells (CELLS) or from
+// `out`, where the scatter pass has put them.
+template <typename T, bool ZZ, bool BUF, int TP, bool CELLS>
 __device__ __forceinline__ void recon_block(const uint16_t* tile, T* out, size_t plane, uint32_t lx, uint32_t nyv,
-                                            uint32_t nzv, size_t base_elem, T r, T ebx2, int lane)
+                                            uint32_t nzv, size_t base_elem, T r, T ebx2, int lane,
+                                            const BrickCells* bc = nullptr)
 {
   T* base = out + base_elem;  // element (x0, y0, z0) of this block
   const __amdgpu_buffer_rsrc_t ro = rsrc(base);
   const uint32_t voff = (uint32_t)lane * sizeof(T);
   const uint32_t l7 = (uint32_t)lane & 7u;
   T s[8];
-#ifndef CUSZ_AMD_RECON_UNROLL
-#define CUSZ_AMD_RECON_UNROLL 8
-#endif
-#pragma unroll CUSZ_AMD_RECON_UNROLL
+#pragma unroll
   for (int y = 0; y < 8; y++) {
     if ((uint32_t)y >= nyv) break;
     uint32_t cd[8];
 #pragma unroll
-    for (int z = 0; z < 8; z++) cd[z] = tile[(y * 8 + z) * kTP + lane];
+    for (int z = 0; z < 8; z++) cd[z] = tile[(y * 8 + z) * TP + lane];
     T v[8];
     bool anyz = false;
 #pragma unroll
@@ -677,11 +698,21 @@ __device__ __forceinline__ void recon_block(const uint16_t* tile, T* out, size_t
         v[z] = (T)cd[z] - r;
       anyz |= cd[z] == 0u;
     }
-#ifndef CUSZ_AMD_RECON_NOOL
-    if (__builtin_amdgcn_ballot_w64(anyz)) {  // outliers: their values were scattered into out
-#else
-    if (false) {  // timing experiment: outliers not read
-#endif
+    if (CELLS && __builtin_amdgcn_ballot_w64(anyz)) {  // outliers: ranked cells of the brick
+#pragma unroll
+      for (int z = 0; z < 8; z++) {
+        const uint64_t m = __builtin_amdgcn_ballot_w64(cd[z] == 0u);
+        if (m && (uint32_t)z < nzv) {
+          const uint32_t row = (uint32_t)y * 8u + (uint32_t)z;
+          const uint32_t c0 = bc->row_start[row] + bc->carry[row], ce = bc->row_start[row + 1];
+          const uint32_t j = c0 + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+          if (cd[z] == 0u) v[z] = (j < ce ? (T)__builtin_bit_cast(float, bc->val[j * bc->vstride]) : T(0)) - r;
+          hfd::wave_sync();
+          if (lane == 0) bc->carry[row] += (uint32_t)__builtin_popcountll(m);
+        }
+      }
+    }
+    else if (!CELLS && __builtin_amdgcn_ballot_w64(anyz)) {  // outliers: their values were scattered into out
       // every row with an outlier is loaded whole (uniform branch), then one wait for all
       T ov[8];
 #pragma unroll
@@ -716,207 +747,64 @@ __device__ __forceinline__ void recon_block(const uint16_t* tile, T* out, size_t
 }
 
 #ifdef CUSZ_AMD_DEC_PROFILE
-// diagnostic build: per-phase clocks and counts summed over waves (psz_amd_debug_brick_profile)
-// 0 bricks, 1 brick cycles, 2 setup cycles, 3 decode cycles, 4 recon cycles, 5 decode loop
-// iterations, 6 fallback lane-steps, 7 idle cycles (work counter), 8 rows loaded
+// diagnostic build (psz_amd_debug_brick_profile): per-phase clocks and counts summed over waves:
+// 0 bricks, 1 brick-start cycles (cells, loads and their wait), 2 decode-loop cycles, 3 drain
+// cycles, 4 reconstruct cycles, 5 loop iterations, 6 lane-quarters sat out for want of data,
+// 7 lane-steps done
 __device__ unsigned long long g_brick_prof[16];
 #define BPROF(...) __VA_ARGS__
 #else
 #define BPROF(...)
 #endif
 
+// Cells of a brick-layout archive: bstart[b] = first cell of brick b (nbricks + 1 entries) and
+// *unsorted != 0 unless the cells are grouped by brick and sorted by (row, x) inside each brick
+// -- key (brick, row = (y % 8) * 8 + z % 8, x % 256) strictly increasing.  bstart and *unsorted
+// are zeroed before the launch.
+__global__ void __launch_bounds__(256) k_brick_cell_bounds(const uint32_t* __restrict__ cells, size_t ncell,
+                                                           uint32_t lx, uint32_t ly, uint32_t lz, uint32_t nbx,
+                                                           uint32_t nby, uint32_t nbricks, uint32_t* bstart,
+                                                           uint32_t* unsorted)
+{
+  auto key = [&](uint32_t idx, uint32_t& brick) -> uint64_t {
+    const uint32_t x = idx % lx, yz = idx / lx, y = yz % ly, z = yz / ly;
+    brick = (z < lz) ? ((z / 8) * nby + y / 8) * nbx + x / 256 : nbricks;
+    return ((uint64_t)brick << 14) | (((y & 7u) * 8u + (z & 7u)) << 8) | (x & 255u);
+  };
+  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < ncell; i += (size_t)gridDim.x * 256) {
+    uint32_t b, bp = 0;
+    const uint64_t k = key(cells[2 * i + 1], b);
+    int64_t prev = -1;
+    if (i > 0) {
+      const uint64_t kp = key(cells[2 * i - 1], bp);
+      if (kp >= k) atomicOr(unsorted, 1u);
+      prev = bp;
+    }
+    if (b >= nbricks) atomicOr(unsorted, 1u);
+    for (int64_t u = prev + 1; u <= (int64_t)b && u <= (int64_t)nbricks; u++) bstart[u] = (uint32_t)i;
+    if (i + 1 == ncell)
+      for (int64_t u = (int64_t)b + 1; u <= (int64_t)nbricks; u++) bstart[u] = (uint32_t)ncell;
+  }
+}
+
 template <typename T, bool ZZ, bool BUF>
-__global__ void __launch_bounds__(64 * kDecMaxWaves)
+__global__ void __launch_bounds__(64 * kDecWaves)
 k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const uint8_t* __restrict__ revbook,
                 int bklen, const uint32_t* __restrict__ par_nbit, const uint32_t* __restrict__ par_entry, T* out,
                 uint32_t lx, uint32_t ly, uint32_t lz, T ebx2, T r, uint32_t nbx, uint32_t nby, uint32_t nbricks,
-                uint32_t ahead, unsigned int* work)
+                BrickOutliers ol)
 {
   __shared__ hfd::LdsTables<kDecB> tb;  // static: table addresses fold into the ds offsets
   extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
   hfd::build_tables<kDecB>(tb, revbook, bklen);
   const hfd::DecRegs rg = hfd::load_dec_regs(tb);
-  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wid: uniform (SGPR)
-  uint32_t* ring = reinterpret_cast<uint32_t*>(dsm + (size_t)wid * kDecWaveBytes);
-  uint16_t* tile = reinterpret_cast<uint16_t*>(ring + kRingWords);
-  // logical ring row L lives in slot kRing - (L % kRing); slot 0 repeats the rows L % kRing == 0,
-  // so rows k + 1 and k always sit in adjacent slots (k + 1 below)
-  const uint32_t* ring_lane = ring + kRing * 64 + lane;
-  const __amdgpu_buffer_rsrc_t rbits =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(bitstream), 0, (int)(bs_words * 4u), (int)kBufRsrcW3);
-  const size_t plane = (size_t)lx * ly;
-  const uint32_t ubk = (uint32_t)bklen;
-  constexpr uint32_t W = 256;
-
-  // bricks are handed out by kWorkShards counters; shard q owns bricks [q per, (q + 1) per)
-  const uint32_t per = (nbricks + kWorkShards - 1) / kWorkShards;
-  const uint32_t q0 = blockIdx.x % kWorkShards;
-  BPROF(unsigned long long pc[9] = {}; unsigned long long tk = __builtin_readcyclecounter(), t0 = tk;)
-  for (uint32_t qi = 0; qi < (uint32_t)kWorkShards;) {
-    const uint32_t q = (q0 + qi) % kWorkShards;
-    uint32_t got = 0;
-    if (lane == 0) got = atomicAdd(work + q * 16, 1u);
-    got = readlane(got, 0);
-    const uint32_t brick = q * per + got;
-    if (got >= per || brick >= nbricks) {
-      qi++;
-      continue;
-    }
-    BPROF(tk = __builtin_readcyclecounter(); pc[7] += tk - t0; t0 = tk; pc[0]++;)
-    const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
-    const uint32_t y0 = by * 8, z0 = bz * 8;
-    const uint32_t ry = (uint32_t)lane >> 3, rz = (uint32_t)lane & 7u;
-    const bool live = y0 + ry < ly && z0 + rz < lz;
-    const size_t c = ((size_t)(z0 + rz) * ly + (y0 + ry)) * nbx + bx;
-    const uint32_t nbit = live ? par_nbit[c] : 0u;
-    const uint32_t ent = live ? par_entry[c] : 0u;
-    const uint32_t voff = ent * 4u;
-    const uint32_t* gsrc = bitstream + ent;
-    const uint32_t glim = bs_words > ent ? bs_words - ent : 1u;
-
-    // initial ring: rows [0, kRing) of every chunk
-    {
-      uint32_t v[kRing];
-#pragma unroll
-      for (uint32_t k = 0; k < kRing; k++) v[k] = __builtin_amdgcn_raw_buffer_load_b32(rbits, (int)voff, (int)(k * 4), 0);
-#pragma unroll
-      for (uint32_t k = 0; k < kRing; k++) ring[(kRing - k) * 64 + lane] = v[k];
-      ring[lane] = v[0];
-    }
-    // per-lane window: rows [ctop - kRing, ctop) resident, rows [ctop, ltop) in flight
-    uint32_t ctop = kRing, ltop = kRing, vt_bits = (kRing - 1u) * 32u;
-    const uint32_t need_top = ((nbit + 31u) >> 5) + 1u;  // the peek pair reads one word past the end
-    uint32_t pos = 0, cnt = live ? 0u : 0x40000000u;  // a dead lane never steps
-    uint32_t pend[kPF];
-    BPROF(hfd::wave_sync(); tk = __builtin_readcyclecounter(); pc[2] += tk - t0; unsigned long long tp = tk;)
-    // Refill, per lane: write the rows loaded at the previous refill into the ring, then load
-    // up to kPF more -- never past the chunk's end, never over a row the lane still needs (row
-    // k replaces row k - kRing; the lane reads from pos / 32 on).
-    auto refill = [&]() {
-#pragma unroll
-      for (int j = 0; j < kPF; j++)
-        if (ctop + j < ltop) {
-          const uint32_t ph = (ctop + j) & (kRing - 1u);
-          ring[(kRing - ph) * 64 + lane] = pend[j];
-          if (ph == 0) ring[lane] = pend[j];
-        }
-      ctop = ltop;
-      vt_bits = (ctop - 1u) * 32u;  // pos >= vt_bits: the word pair at pos is not resident
-      const uint32_t lim = min(need_top, (pos >> 5) + kRing - 1u);
-      const uint32_t nload = lim > ltop ? min(lim - ltop, (uint32_t)kPF) : 0u;
-      const uint32_t lvoff = voff + ltop * 4u;
-#pragma unroll
-      for (int j = 0; j < kPF; j++)
-        if ((uint32_t)j < nload) pend[j] = __builtin_amdgcn_raw_buffer_load_b32(rbits, (int)lvoff, j * 4, 0);
-      BPROF(pc[8] += wave_sum64(nload);)
-      ltop += nload;
-    };
-
-    for (int blk = 0; blk < (int)(W / kBlk); blk++) {
-      uint16_t* rowp = tile + lane * kTP - blk * kBlk;  // rowp[cnt] = tile column cnt - 64 blk
-      const uint32_t target = (uint32_t)(blk + 1) * kBlk;
-      refill();
-      uint32_t it = 0;
-      do {
-#pragma unroll
-        for (int st = 0; st < kSteps; st++)
-          if (cnt < target) {
-            // rows k and k + 1 are adjacent slots, k + 1 below k: one ds_read2 gives {w1, w0}
-            const uint32_t* pr = ring_lane - ((pos >> 5) & (kRing - 1u)) * 64;
-            uint32_t w1 = pr[-64], w0 = pr[0];
-            if (__builtin_expect(pos >= vt_bits, 0)) {
-              fallback_pair(gsrc, pos >> 5, glim, w0, w1);
-              BPROF(pc[6]++;)
-            }
-            const uint64_t pair = ((uint64_t)w0 << 32) | w1;
-            const uint32_t win = (uint32_t)((pair << (pos & 31u)) >> 32);  // chunk bits [pos, pos + 32)
-            const uint32_t e = hfd::lookup<kDecB>(tb, rg, win, ubk);
-            // both symbols with one (2-B aligned) 32-bit store; the second is overwritten next
-            // step unless the entry holds two
-            *reinterpret_cast<uint32_t*>(rowp + cnt) = e & hfd::kEntSymMask;
-            pos += hfd::ent_bits(e);
-            cnt += hfd::ent_nsym(e);
-          }
-        BPROF(pc[5]++;)
-        if ((++it & (kRefillEvery - 1)) == 0) refill();
-      } while (__builtin_amdgcn_ballot_w64(cnt < target));
-      hfd::wave_sync();
-      BPROF(tk = __builtin_readcyclecounter(); pc[3] += tk - tp; tp = tk;)
-      {
-        const uint32_t nyv = min(8u, ly - y0), nzv = min(8u, lz - z0);
-        const size_t base_elem = (size_t)z0 * plane + (size_t)y0 * lx + (size_t)bx * W + (size_t)blk * kBlk;
-        recon_block<T, ZZ, BUF>(tile, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane);
-      }
-      hfd::wave_sync();
-      BPROF(tk = __builtin_readcyclecounter(); pc[4] += tk - tp; tp = tk;)
-      // a two-symbol step that crossed the block end left the next block's first symbol in
-      // column 64
-      if (cnt == (uint32_t)(blk + 1) * kBlk + 1u) tile[lane * kTP] = tile[lane * kTP + kBlk];
-      hfd::wave_sync();
-    }
-    BPROF(tk = __builtin_readcyclecounter(); pc[1] += tk - t0; t0 = tk;)
-  }
-#ifdef CUSZ_AMD_DEC_PROFILE
-  pc[6] = wave_sum64(pc[6]);
-  if (lane == 0)
-    for (int i = 0; i < 9; i++) atomicAdd(&g_brick_prof[i], pc[i]);
-#endif
-}
-
-// =========================================================================================
-// decompress v2: register bit window, counted refills
-// =========================================================================================
-// Same work split as k_brick3_decode (one wave per brick, lane l decodes chunk l = brick row
-// (l / 8, l % 8) in blocks of 64 symbols, the block reconstructed with lane = column), but the
-// decode step keeps its bits in registers: w0:w1 is a 64-bit window (`sh` = 32 - bits consumed
-// of w0, so the next 32 chunk bits are alignbit(w0, w1, sh)), w2 and nx are the next two words.
-// A step is one table lookup (the only LDS round trip on the chain); when it crosses a word
-// boundary the words shift down and nx is refilled from the lane's LDS ring (word k in slot
-// k % kR2, [slot][lane]).  The ring is refilled every kF2 steps: each lane issues one 16-B load
-// of its next four words (or an out-of-range load that returns nothing) and writes the group it
-// loaded two refills earlier, so a load has 2 kF2 steps to land and the wait for it is a counted
-// vmcnt(1) -- never behind the reconstruction's stores, which are only issued after the ring
-// has been drained at the block's end.  A lane whose next word has not landed yet sits out
-// steps (its predicate is off) until it has; nothing ever waits in the step loop.
-#ifndef CUSZ_AMD_DEC2_F
-#define CUSZ_AMD_DEC2_F 8
-#endif
-#ifndef CUSZ_AMD_DEC2_WAVES
-#define CUSZ_AMD_DEC2_WAVES 8
-#endif
-constexpr int kF2 = CUSZ_AMD_DEC2_F;  // decode steps between ring refills
-constexpr uint32_t kR2 = 16;          // ring words per lane (power of two)
-constexpr size_t kDec2WaveBytes = (size_t)(kR2 + 1) * 64 * 4 + (size_t)64 * kTP * 2;  // ring + junk slot + tile
-constexpr int kDec2Waves = CUSZ_AMD_DEC2_WAVES;
-#ifndef CUSZ_AMD_DEC2_DBG
-#define CUSZ_AMD_DEC2_DBG 0
-#endif
-// timing experiments only (wrong output): 1 no reconstruction, 2 no tile stores, 4 L1 lookup
-// only, 8 every lane steps every step, 16 no ring reads
-constexpr int kDec2Dbg = CUSZ_AMD_DEC2_DBG;
-#ifndef CUSZ_AMD_DEC2_STEP_UNROLL
-#define CUSZ_AMD_DEC2_STEP_UNROLL 8
-#endif
-#ifndef CUSZ_AMD_DEC2_L2COND
-#define CUSZ_AMD_DEC2_L2COND 0
-#endif
-constexpr bool kDec2L2Cond = CUSZ_AMD_DEC2_L2COND;  // L2 table read only for the lanes L1 missed
-constexpr uint32_t kOOB = 0x80000000u;  // buffer offset past any bitstream: the load returns 0
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-template <typename T, bool ZZ, bool BUF>
-__global__ void __launch_bounds__(64 * kDec2Waves)
-k_brick3_decode2(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const uint8_t* __restrict__ revbook,
-                 int bklen, const uint32_t* __restrict__ par_nbit, const uint32_t* __restrict__ par_entry, T* out,
-                 uint32_t lx, uint32_t ly, uint32_t lz, T ebx2, T r, uint32_t nbx, uint32_t nby, uint32_t nbricks)
-{
-  __shared__ hfd::LdsTables<kDecB> tb;
-  extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
-  hfd::build_tables<kDecB>(tb, revbook, bklen);
-  const hfd::DecRegs rg = hfd::load_dec_regs(tb);
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint32_t* ring_lane = reinterpret_cast<uint32_t*>(dsm + (size_t)wid * kDec2WaveBytes) + lane;
-  uint16_t* tile = reinterpret_cast<uint16_t*>(dsm + (size_t)wid * kDec2WaveBytes + (size_t)(kR2 + 1) * 64 * 4);
+  uint8_t* wbase = dsm + (size_t)wid * kDecWaveBytes;
+  uint32_t* ring_lane = reinterpret_cast<uint32_t*>(wbase) + lane;
+  uint16_t* tile = reinterpret_cast<uint16_t*>(wbase + kDecTile);
+  uint32_t* cval = reinterpret_cast<uint32_t*>(wbase + kDecCells);
+  BrickCells bc{cval, 1, reinterpret_cast<uint32_t*>(wbase + kDecRows), reinterpret_cast<uint32_t*>(wbase + kDecRows) + 65};
+  const bool ranked = !ZZ && (ol.ncell == 0 || !*ol.unsorted);
   const __amdgpu_buffer_rsrc_t rbits =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(bitstream), 0, (int)(bs_words * 4u), (int)kBufRsrcW3);
   const size_t plane = (size_t)lx * ly;
@@ -925,9 +813,6 @@ k_brick3_decode2(const uint32_t* __restrict__ bitstream, uint32_t bs_words, cons
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
   const uint32_t ry = (uint32_t)lane >> 3, rz = (uint32_t)lane & 7u;
 
-  // diagnostic build (psz_amd_debug_brick_profile): 0 bricks, 1 brick-start cycles (loads and
-  // their wait), 2 decode-loop cycles, 3 drain cycles, 4 reconstruct cycles, 5 loop iterations,
-  // 6 lane-steps skipped for want of data, 7 lane-steps done
   BPROF(unsigned long long pc[8] = {}; unsigned long long tk = __builtin_readcyclecounter(), tp = tk;)
   for (uint32_t brick = blockIdx.x * (blockDim.x >> 6) + wid; brick < nbricks; brick += nw) {
     BPROF(pc[0]++; tp = __builtin_readcyclecounter();)
@@ -938,42 +823,57 @@ k_brick3_decode2(const uint32_t* __restrict__ bitstream, uint32_t bs_words, cons
     const uint32_t nbit = live ? par_nbit[c] : 0u;
     const uint32_t vbase = (live ? par_entry[c] : 0u) * 4u;
     const uint32_t nwords = (nbit + 31u) >> 5;
-    // words 0..7: 0..2 into registers, 3..7 into the ring
-    uint32_t w0 = 0, w1, w2, nx;
-    {
-      const u32x4 a0 = __builtin_amdgcn_raw_buffer_load_b128(rbits, (int)(live ? vbase : kOOB), 0, 0);
-      const u32x4 a1 = __builtin_amdgcn_raw_buffer_load_b128(rbits, (int)(live ? vbase + 16u : kOOB), 0, 0);
-      w1 = a0.x, w2 = a0.y, nx = a0.z;
-      ring_lane[3 * 64] = a0.w;
-      ring_lane[4 * 64] = a1.x, ring_lane[5 * 64] = a1.y, ring_lane[6 * 64] = a1.z, ring_lane[7 * 64] = a1.w;
+    // words 0..7 (0..2 into registers, 3..7 into the ring), issued before the cells are read
+    const u32x4 a0 = __builtin_amdgcn_raw_buffer_load_b128(rbits, (int)(live ? vbase : kOOB), 0, 0);
+    const u32x4 a1 = __builtin_amdgcn_raw_buffer_load_b128(rbits, (int)(live ? vbase + 16u : kOOB), 0, 0);
+    // the brick's outlier cells [cb, ce): per-row counts -> row starts; values into LDS
+    if (ranked) {
+      uint32_t cb = 0, ce = 0;
+      if (ol.ncell) cb = ol.bstart[brick], ce = ol.bstart[brick + 1];
+      const uint32_t nc = ce - cb;
+      bc.row_start[lane] = 0;
+      hfd::wave_sync();
+      for (uint32_t j = (uint32_t)lane; j < nc; j += 64) {
+        const uint32_t idx = ol.cells[2 * (cb + j) + 1];
+        const uint32_t yz = idx / lx;  // y + ly z
+        atomicAdd(&bc.row_start[((yz % ly) & 7u) * 8u + ((yz / ly) & 7u)], 1u);
+        if (nc <= kCellCap) cval[j] = ol.cells[2 * (cb + j)];
+      }
+      hfd::wave_sync();
+      const uint32_t cr = bc.row_start[lane];
+      const uint32_t incl = hfd::wave_incl_scan(cr);
+      bc.row_start[lane] = incl - cr;
+      if (lane == 63) bc.row_start[64] = incl;
+      bc.carry[lane] = 0;
+      bc.val = nc <= kCellCap ? cval : ol.cells + 2 * (size_t)cb;
+      bc.vstride = nc <= kCellCap ? 1u : 2u;
     }
-    uint32_t kk = 2;           // word index held by nx
-    uint32_t ctop = 8;         // words [0, ctop) have been written (ring or registers)
-    uint32_t ltop = 8;         // words [0, ltop) have been requested
-    uint32_t sh = 0;           // 32 - bits of w0 consumed
-    uint32_t cnt = live ? 0u : 0x40000000u;  // a dead lane never steps
-    uint32_t keep = 0;         // symbol at the even column before an odd cnt (see the tile stores)
-    uint32_t rdy = ctop >= nwords ? 0xFFFFFFFFu : ctop;  // the lane steps while kk + 1 < rdy
-    u32x4 pa, pb;              // groups in flight (loaded one / two refills ago)
+    uint32_t w0 = 0, w1 = a0.x, w2 = a0.y, nx = a0.z;
+    ring_lane[3 * 64] = a0.w;
+    ring_lane[4 * 64] = a1.x, ring_lane[5 * 64] = a1.y, ring_lane[6 * 64] = a1.z, ring_lane[7 * 64] = a1.w;
+    uint32_t kk = 2;    // word index held by nx
+    uint32_t ctop = 8;  // words [0, ctop) have been written (ring or registers)
+    uint32_t ltop = 8;  // words [0, ltop) have been requested
+    uint32_t sh = 0;    // 32 - bits of w0 consumed
+    uint32_t cnt = live ? 0u : 0x40000000u;  // symbols decoded; a dead lane never steps
+    uint32_t keep = 0;  // symbol at the even column before an odd cnt (see the tile stores)
+    uint32_t rdy = ctop >= nwords ? 0xFFFFFFFFu : ctop;  // words [0, rdy) are readable
+    u32x4 pa, pb;       // groups in flight
     bool fa = false, fb = false;
-
     BPROF(hfd::wave_sync(); tk = __builtin_readcyclecounter(); pc[1] += tk - tp; tp = tk;)
+
     auto issue = [&](u32x4& p, bool& f) {
-      const bool ok = ltop < nwords && ltop + 4u <= kk + kR2;
+      const bool ok = ltop < nwords && ltop + 4u <= kk + kRing;  // never over a word still needed
       p = __builtin_amdgcn_raw_buffer_load_b128(rbits, (int)(ok ? vbase + ltop * 4u : kOOB), 0, 0);
       f = ok;
       ltop += ok ? 4u : 0u;
     };
     // Write a landed group into the ring.  The stores are unconditional (a lane without a group
-    // writes the junk slot kR2), so the compiler's wait for the load sits here on every path and
+    // writes the junk slot kRing), so the compiler's wait for the load sits here on every path and
     // no load is left pending past the block's end.
     auto consume = [&](const u32x4& p, bool& f) {
-      const uint32_t s0 = f ? ctop : kR2 * 4u;  // kR2 * 4: every word goes to slot kR2
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const uint32_t slot = f ? ((s0 + (uint32_t)i) & (kR2 - 1u)) : kR2;
-        ring_lane[slot * 64] = p[i];
-      }
+      for (int i = 0; i < 4; i++) ring_lane[(f ? ((ctop + (uint32_t)i) & (kRing - 1u)) : kRing) * 64] = p[i];
       ctop += f ? 4u : 0u;
       f = false;
       rdy = ctop >= nwords ? 0xFFFFFFFFu : ctop;
@@ -982,66 +882,43 @@ k_brick3_decode2(const uint32_t* __restrict__ bitstream, uint32_t bs_words, cons
     for (int blk = 0; blk < (int)(W / kBlk); blk++) {
       uint16_t* rowp = tile + lane * kTP - blk * kBlk;  // rowp[cnt] = tile column cnt - 64 blk
       const uint32_t target = (uint32_t)(blk + 1) * kBlk;
-      auto steps = [&]() {
-#pragma unroll CUSZ_AMD_DEC2_STEP_UNROLL
-        for (int st = 0; st < kF2; st++) {
-          BPROF(pc[6] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(cnt < target && !(kk + 1u < rdy)));
-                pc[7] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(cnt < target && kk + 1u < rdy));)
-          if ((kDec2Dbg & 8) || (cnt < target && kk + 1u < rdy)) {
+      auto quarter = [&]() {
+        BPROF(pc[6] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(cnt < target && !(kk + (uint32_t)kF < rdy)));
+              pc[7] += kF * __builtin_popcountll(__builtin_amdgcn_ballot_w64(cnt < target && kk + (uint32_t)kF < rdy));)
+        if (cnt < target && kk + (uint32_t)kF < rdy) {
+#pragma unroll
+          for (int st = 0; st < kF; st++) {
             const uint32_t win = __builtin_amdgcn_alignbit(w0, w1, sh);  // chunk bits [pos, pos + 32)
-            uint32_t e;
-            if constexpr (kDec2Dbg & 4)
-              e = tb.l1[win >> (32 - kDecB)] | 0x04000000u;
-            else if constexpr (kDec2L2Cond)
-              e = hfd::lookup_l1_first<kDecB>(tb, rg, win, ubk);
-            else
-              e = hfd::lookup<kDecB>(tb, rg, win, ubk);
-            // symbols go to the tile as aligned u32 pairs: at an even column the entry's two
-            // symbols (the second is overwritten next step unless the entry holds two); at an odd
-            // column the symbol kept from the previous step and this step's first.  `keep` then
-            // holds the symbol the next odd-column store needs.
-            {
-              const uint32_t sy = e & hfd::kEntSymMask;
-              const bool odd = cnt & 1u;
-              const uint32_t word = odd ? (keep | (sy << 16)) : sy;
-              if constexpr (!(kDec2Dbg & 2)) *reinterpret_cast<uint32_t*>(rowp + (cnt & ~1u)) = word;
-              keep = odd ? (sy >> 16) : (sy & 0xFFFFu);
-            }
+            const uint32_t e = hfd::lookup<kDecB>(tb, rg, win, ubk);
+            const uint32_t sy = e & hfd::kEntSymMask;
+            const bool odd = cnt & 1u;
+            *reinterpret_cast<uint32_t*>(rowp + (cnt & ~1u)) = odd ? (keep | (sy << 16)) : sy;
+            keep = odd ? (sy >> 16) : (sy & 0xFFFFu);
             cnt += hfd::ent_nsym(e);
             const int32_t s2 = (int32_t)sh - (int32_t)hfd::ent_bits(e);
-            const bool shf = s2 < 0;
+            const bool shf = s2 < 0;  // crossed into the next word
             sh = (uint32_t)s2 & 31u;
-            if constexpr (kDec2Dbg & 64) {  // branch-free shift, nx re-read every step
-              w0 = shf ? w1 : w0;
-              w1 = shf ? w2 : w1;
-              w2 = shf ? nx : w2;
-              kk += shf ? 1u : 0u;
-              nx = ring_lane[(kk & (kR2 - 1u)) * 64];
-            }
-            else if (shf) {  // crossed into the next word: shift, refill nx from the ring
-              w0 = w1, w1 = w2, w2 = nx;
-              kk++;
-              if constexpr (kDec2Dbg & 16)
-                nx = nx * 0x9E3779B9u + kk;
-              else
-                nx = ring_lane[(kk & (kR2 - 1u)) * 64];
-            }
+            w0 = shf ? w1 : w0;
+            w1 = shf ? w2 : w1;
+            w2 = shf ? nx : w2;
+            kk += shf ? 1u : 0u;
+            nx = ring_lane[(kk & (kRing - 1u)) * 64];
           }
         }
       };
       // a group is written into the ring two refills after its load; the first wait of a block
-      // comes 2 kF2 steps after the previous block's stores
+      // comes 2 kF steps after the previous block's stores
       issue(pa, fa);
-      steps();
+      quarter();
       issue(pb, fb);
-      steps();
+      quarter();
       do {
         consume(pa, fa);
         issue(pa, fa);
-        steps();
+        quarter();
         consume(pb, fb);
         issue(pb, fb);
-        steps();
+        quarter();
         BPROF(pc[5]++;)
       } while (__builtin_amdgcn_ballot_w64(cnt < target));
       BPROF(hfd::wave_sync(); tk = __builtin_readcyclecounter(); pc[2] += tk - tp; tp = tk;)
@@ -1052,12 +929,23 @@ k_brick3_decode2(const uint32_t* __restrict__ bitstream, uint32_t bs_words, cons
       {
         const uint32_t nyv = min(8u, ly - y0), nzv = min(8u, lz - z0);
         const size_t base_elem = (size_t)z0 * plane + (size_t)y0 * lx + (size_t)bx * W + (size_t)blk * kBlk;
-        if constexpr (!(kDec2Dbg & 1)) recon_block<T, ZZ, BUF>(tile, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane);
+        if (ranked)
+          recon_block<T, ZZ, BUF, kTP, true>(tile, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane, &bc);
+        else
+          recon_block<T, ZZ, BUF, kTP, false>(tile, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane);
+      }
+      hfd::wave_sync();
+      // symbols decoded past the block end move to its front (`keep` carries a pending one)
+      {
+        uint32_t* rw = reinterpret_cast<uint32_t*>(tile + lane * kTP);
+        uint32_t v[kF];
+#pragma unroll
+        for (int i = 0; i < kF; i++) v[i] = rw[kBlk / 2 + i];
+#pragma unroll
+        for (int i = 0; i < kF; i++) rw[i] = v[i];
       }
       hfd::wave_sync();
       BPROF(tk = __builtin_readcyclecounter(); pc[4] += tk - tp; tp = tk;)
-      // (a two-symbol step that crossed the block end keeps the next block's first symbol in
-      // `keep`: cnt is odd, so the next block's first store writes it to column 0)
     }
   }
 #ifdef CUSZ_AMD_DEC_PROFILE
@@ -1065,7 +953,6 @@ k_brick3_decode2(const uint32_t* __restrict__ bitstream, uint32_t bs_words, cons
     for (int i = 0; i < 8; i++) atomicAdd(&g_brick_prof[i], pc[i]);
 #endif
 }
-
 }  // namespace
 
 // =========================================================================================
@@ -1088,16 +975,6 @@ BrickGeom brick_geom(int ndim, size_t lx, size_t ly, size_t lz, int elem_bytes)
   g.nchunks = (uint32_t)(lx / g.W * ly * lz);
   return g;
 }
-
-// total LDS (static tables + dynamic per-wave ring and tile) of the fused decoder
-size_t brick_decode_lds(int waves)
-{
-  const size_t tab = (sizeof(hfd::LdsTables<kDecB>) + 15) / 16 * 16;
-  return tab + (size_t)waves * kDecWaveBytes;
-}
-
-uint32_t brick_decode_max_ahead() { return kRing - 1; }
-int brick_decode_max_waves() { return kDecMaxWaves; }
 
 int brick_configure(BrickLaunch& L, int elem_bytes, int device)
 {
@@ -1170,42 +1047,35 @@ int launch_brick_pack(const BrickLaunch& L, const uint16_t* bcodes, const uint32
   return (int)hipGetLastError();
 }
 
+int launch_brick_cell_bounds(const BrickLaunch& L, const uint32_t* cells, size_t ncell, uint32_t* bstart,
+                             uint32_t* unsorted, hipStream_t st)
+{
+  if (!ncell) return (int)hipSuccess;
+  const uint32_t grid = (uint32_t)std::min<size_t>((ncell + 255) / 256, 2048);
+  k_brick_cell_bounds<<<grid, 256, 0, st>>>(cells, ncell, L.lx, L.ly, L.lz, L.g.nbx, L.g.nby, L.g.nbricks, bstart,
+                                            unsorted);
+  return (int)hipGetLastError();
+}
+
 template <typename T>
 int launch_brick_decode(const BrickLaunch& L, const uint32_t* bitstream, size_t bs_words, const uint8_t* revbook,
                         int bklen, const uint32_t* par_nbit, const uint32_t* par_entry, T* out, double eb, int radius,
-                        bool zz, uint32_t ahead, int waves, unsigned int* work, hipStream_t st)
+                        bool zz, const BrickOutliers& ol, hipStream_t st)
 {
   const T ebx2 = (T)(eb * 2);  // lrz_x.cuhip.inl:432
   const T r = (T)radius;
   const BrickGeom& g = L.g;
+  static_assert(sizeof(hfd::LdsTables<kDecB>) + kDecWaves * kDecWaveBytes <= 160 * 1024, "LDS");
   if (bs_words >= (1ull << 30)) return (int)hipErrorInvalidValue;
-  const int grid = L.ncu;
   // buffer stores address a brick block with 32-bit offsets from its first element
   const size_t plane = (size_t)L.lx * L.ly;
   const bool buf = (7 * plane + 7 * (size_t)L.lx + (size_t)kBlk) * sizeof(T) < (1ull << 31);
   const uint32_t bw = (uint32_t)bs_words;
-  static const bool v1 = getenv("CUSZ_AMD_BRICK_DEC_V1") != nullptr;  // TEMP: A/B of the two decoders
-  if (!v1) {
-    const size_t lds = (size_t)kDec2Waves * kDec2WaveBytes;
-#define DEC2_LAUNCH(ZZ, BUF)                                                                                        \
-  k_brick3_decode2<T, ZZ, BUF><<<grid, 64 * kDec2Waves, lds, st>>>(bitstream, bw, revbook, bklen, par_nbit, par_entry, \
-                                                                   out, L.lx, L.ly, L.lz, ebx2, r, g.nbx, g.nby,      \
-                                                                   g.nbricks)
-    if (zz) {
-      if (buf) DEC2_LAUNCH(true, true); else DEC2_LAUNCH(true, false);
-    }
-    else {
-      if (buf) DEC2_LAUNCH(false, true); else DEC2_LAUNCH(false, false);
-    }
-#undef DEC2_LAUNCH
-    return (int)hipGetLastError();
-  }
-  if (brick_decode_lds(waves) > 160 * 1024 || waves < 1 || waves > kDecMaxWaves) return (int)hipErrorInvalidValue;
-  const size_t lds = (size_t)waves * kDecWaveBytes;  // dynamic part
-#define DEC_LAUNCH(ZZ, BUF)                                                                                       \
-  k_brick3_decode<T, ZZ, BUF><<<grid, 64 * waves, lds, st>>>(bitstream, bw, revbook, bklen, par_nbit, par_entry, out, \
-                                                             L.lx, L.ly, L.lz, ebx2, r, g.nbx, g.nby, g.nbricks,      \
-                                                             ahead, work)
+  const size_t lds = (size_t)kDecWaves * kDecWaveBytes;  // dynamic part
+#define DEC_LAUNCH(ZZ, BUF)                                                                                     \
+  k_brick3_decode<T, ZZ, BUF><<<L.ncu, 64 * kDecWaves, lds, st>>>(bitstream, bw, revbook, bklen, par_nbit, par_entry, \
+                                                                  out, L.lx, L.ly, L.lz, ebx2, r, g.nbx, g.nby,       \
+                                                                  g.nbricks, ol)
   if (zz) {
     if (buf) DEC_LAUNCH(true, true); else DEC_LAUNCH(true, false);
   }
@@ -1232,8 +1102,8 @@ extern "C" int psz_amd_debug_brick_profile(unsigned long long* host, int reset)
   template int launch_brick_scan<T>(const BrickLaunch&, const T*, double, int, bool, const OutlierSink&, uint32_t*, \
                                     uint16_t*, uint16_t*, int, hipStream_t);                                       \
   template int launch_brick_decode<T>(const BrickLaunch&, const uint32_t*, size_t, const uint8_t*, int,            \
-                                      const uint32_t*, const uint32_t*, T*, double, int, bool, uint32_t, int,       \
-                                      unsigned int*, hipStream_t);
+                                      const uint32_t*, const uint32_t*, T*, double, int, bool, const BrickOutliers&, \
+                                      hipStream_t);
 INST(float)
 INST(double)
 #undef INST

@@ -202,11 +202,6 @@ struct BrickLaunch {
 // fills ncu and the encode-pass grids for `device`
 int brick_configure(BrickLaunch& L, int elem_bytes, int device);
 
-// LDS bytes of the fused decoder for `waves` waves; the largest look-ahead (ring rows) it takes
-size_t brick_decode_lds(int waves);
-uint32_t brick_decode_max_ahead();
-int brick_decode_max_waves();
-
 // pass 1: predict -> global + per-brick histograms, outliers, codes in brick order (bcodes:
 // nbricks * 64 rows * W u16)
 template <typename T>
@@ -243,10 +238,22 @@ int launch_brick_plan(const BrickLaunch& L, const BrickPlanArgs& a, const void* 
 int launch_brick_pack(const BrickLaunch& L, const uint16_t* bcodes, const uint32_t* book, int bklen,
                       const BrickPlanArgs& plan, uint32_t* par_nbit, uint32_t* par_entry, uint32_t* bitstream,
                       int reverse, unsigned int* overflow, hipStream_t st);
+// Outlier cells for the fused decoder: when the archive's cells are grouped by brick and sorted
+// by (row, x) (k_brick_cell_bounds checks; this compressor writes them so), the decoder ranks the
+// zero codes of each row against the brick's cells and no scatter pass is needed; otherwise
+// (*unsorted set) the scatter pass has written the values into `out`, which the decoder reads.
+struct BrickOutliers {
+  const uint32_t* cells = nullptr;  // archive cells {f32 value, u32 idx}
+  size_t ncell = 0;
+  const uint32_t* bstart = nullptr;   // nbricks + 1
+  const uint32_t* unsorted = nullptr;
+};
+int launch_brick_cell_bounds(const BrickLaunch& L, const uint32_t* cells, size_t ncell, uint32_t* bstart,
+                             uint32_t* unsorted, hipStream_t st);
 template <typename T>
 int launch_brick_decode(const BrickLaunch& L, const uint32_t* bitstream, size_t bs_words, const uint8_t* revbook,
                         int bklen, const uint32_t* par_nbit, const uint32_t* par_entry, T* out, double eb, int radius,
-                        bool zz, uint32_t ahead, int waves, unsigned int* work, hipStream_t st);
+                        bool zz, const BrickOutliers& ol, hipStream_t st);
 
 // min / max (Rel mode, extrema.cuhip.inl:86-208), writes {min, max} as doubles
 template <typename T>

@@ -138,8 +138,7 @@ struct Pipeline {
   double* minmax() { return reinterpret_cast<double*>(d_small + 256); }
   unsigned int* ext_scratch() { return reinterpret_cast<unsigned int*>(d_small + 512); }
   uint32_t* dec_lut() { return reinterpret_cast<uint32_t*>(d_small + 512 + 2 * 1024 * 8); }
-  static constexpr size_t kWorkBytes = 512;  // fused decoder work counters (8 shards x 64 B)
-  static constexpr size_t kSmallBytes = 512 + 2 * 1024 * 8 + kHfDecScratchWords * 4 + kWorkBytes;
+  static constexpr size_t kSmallBytes = 512 + 2 * 1024 * 8 + kHfDecScratchWords * 4;
 
   ~Pipeline() { release(); }
 
@@ -169,7 +168,6 @@ struct Pipeline {
     const uint32_t nu = brick_units(bl.g.nbricks), per = (bl.g.nbricks + nu - 1) / nu;
     return (uint32_t)((size_t)bl.g.brick_elems * per / 10 + 16);
   }
-  unsigned int* work_counter() { return reinterpret_cast<unsigned int*>(d_small + kSmallBytes - kWorkBytes); }
 
   // fused brick path: 3-D, eligible shape, Lorenzo, default chunking (chunk = brick row)
   bool use_brick(psz_predictor pred) const
@@ -212,6 +210,8 @@ struct Pipeline {
       CUSZ_AMD_HIP_CHECK(hipMalloc(&d_ub, (size_t)bl.g.nbricks * 4));
       CUSZ_AMD_HIP_CHECK(hipMalloc(&d_bbase, ((size_t)bl.g.nbricks + 1) * 4));
       CUSZ_AMD_HIP_CHECK(hipMalloc(&d_plan, 2 * ((size_t)brick_plan_blocks(bl.g.nbricks) + 1) * 4));
+      // fused decompression: per-brick first outlier cell + unsorted flag (d_x1d's role in 1-D)
+      if (!d_x1d) CUSZ_AMD_HIP_CHECK(hipMalloc(&d_x1d, ((size_t)bl.g.nbricks + 2) * 4));
     }
 
     // codes: index order (reference layout) or brick order (brick layout: whole bricks)
@@ -639,10 +639,20 @@ struct Pipeline {
       CUSZ_AMD_HIP_CHECK((hipError_t)launch_x1d_bounds(cells, h->splen, n, nb, d_x1d, d_x1d + nb + 1, stream));
       ox = X1dOutliers{cells, (size_t)h->splen, d_x1d, d_x1d + nb + 1};
     }
+    // fused brick path: the decoder ranks each row's zero codes against the brick's cells when
+    // they are grouped and sorted; only otherwise does the scatter below run (only_if = unsorted)
+    BrickOutliers bo;
+    if (brickdec && !zz && h->splen) {
+      const uint32_t nb = bl.g.nbricks;
+      CUSZ_AMD_HIP_CHECK(hipMemsetAsync(d_x1d, 0, ((size_t)nb + 2) * 4, stream));
+      CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_cell_bounds(bl, cells, h->splen, d_x1d, d_x1d + nb + 1, stream));
+      bo = BrickOutliers{cells, (size_t)h->splen, d_x1d, d_x1d + nb + 1};
+      ox.unsorted = bo.unsorted;
+    }
     if (zz) CUSZ_AMD_HIP_CHECK(hipMemsetAsync(out, 0, n * sizeof(T), stream));
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_scatter<T>(cells, h->splen, out, n, stream, ox.unsorted));
     mark(7);
-    if (brickdec) return decompress_brick<T>(h, in, out, zz);
+    if (brickdec) return decompress_brick<T>(h, in, out, zz, bo);
     int s = decode_codes(h, in);
     if (s) return s;
     mark(8);
@@ -654,32 +664,21 @@ struct Pipeline {
 
   // fused decode + reconstruct (brick.hip): any archive whose chunk length is the brick width
   template <typename T>
-  int decompress_brick(const psz_header* h, const uint8_t* in, T* out, bool zz)
+  int decompress_brick(const psz_header* h, const uint8_t* in, T* out, bool zz, const BrickOutliers& bo)
   {
     const int bklen = 2 * h->rc.radius;
     const size_t phf_off = h->entry[PSZHEADER_ENCODED];
     const size_t rvbk = rvbk_bytes(bklen);
     const int pd = h->vle_pardeg;
     const uint8_t* phf = in + phf_off;
-    const size_t seg = h->entry[PSZHEADER_ENCODED + 1] - h->entry[PSZHEADER_ENCODED];
-    const size_t fixed = 128 + rvbk + 8 * (size_t)pd;
-    const size_t cells = seg > fixed ? (seg - fixed) / 4 : 0;
-    // ring rows prefetched past the fastest lane: about two sub-blocks (32 symbols) of words at
-    // the archive's average bits per symbol
-    const double words_per_sub = (double)cells / std::max<size_t>(pd, 1) * 32.0 / bl.g.W;
-    uint32_t ahead = (uint32_t)(2.5 * words_per_sub) + 3;
-    ahead = std::min(ahead, brick_decode_max_ahead());
-    int waves = brick_decode_max_waves();
-    while (waves > 1 && brick_decode_lds(waves) > 160 * 1024) waves--;
     // words from the bitstream start to the end of the archive (range of the decoder's loads)
     const size_t bits_off = phf_off + 128 + rvbk + 8 * (size_t)pd;
     const size_t total = h->entry[PSZHEADER_ENC_PASS2_END];
     const size_t bs_words = total > bits_off ? (total - bits_off) / 4 : 0;
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_zero(regions({{work_counter(), nullptr, kWorkBytes}}), stream));
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_decode<T>(
         bl, reinterpret_cast<const uint32_t*>(phf + 128 + rvbk + 8 * (size_t)pd), bs_words, phf + 128, bklen,
         reinterpret_cast<const uint32_t*>(phf + 128 + rvbk), reinterpret_cast<const uint32_t*>(phf + 128 + rvbk + 4 * (size_t)pd),
-        out, h->rc.eb, h->rc.radius, zz, ahead, waves, work_counter(), stream));
+        out, h->rc.eb, h->rc.radius, zz, bo, stream));
     mark(8);
     mark(9);
     return PSZ_SUCCESS;

@@ -1,9 +1,8 @@
 #!/usr/bin/env python3
 """Micro-benchmark of the fused brick kernels on a config-2 field (512^3 f32, abs 1e-4).
 
-Times compress and decompress with HIP events on the manager's stream, and decompress again
-under the decoder's diagnostic switch CUSZ_AMD_DEC_DEBUG (1: skip the decode loop, 2: skip the
-reconstruction, 3: both) to split the fused decoder's time.
+Times compress and decompress with HIP events on the manager's stream (CUSZ_AMD_LIB selects a
+variant library, e.g. one built with a timing-experiment switch).
 Usage: python scripts/brick_bench.py [--dims 512x512x512] [--reps 10] [--f64]
 """
 import argparse
@@ -25,7 +24,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--eb", type=float, default=1e-4)
     ap.add_argument("--f64", action="store_true")
-    ap.add_argument("--dbg", default="1,2,3,0", help="decoder diagnostic variants to time, in order")
+    ap.add_argument("--dbg", default="0", help="(ignored; kept for old command lines)")
     a = ap.parse_args()
     dims = tuple(int(v) for v in a.dims.split("x"))
     dt = torch.float64 if a.f64 else torch.float32
@@ -53,10 +52,8 @@ def main():
     stc = r.stage_times()
     ptr, nb, _ = r.compress(d_in.data_ptr(), a.eb)
     torch.cuda.synchronize()
-    for dbg in a.dbg.split(","):
-        os.environ["CUSZ_AMD_DEC_DEBUG"] = dbg
-        td = timeit(lambda: r.decompress(ptr, nb, out.data_ptr()))
-        print(f"decompress dbg={dbg}: {td * 1e3:.1f} us")
+    td = timeit(lambda: r.decompress(ptr, nb, out.data_ptr()))
+    print(f"decompress dbg=0: {td * 1e3:.1f} us")
     err = (out.double() - d_in.double()).abs().max().item()
     gb = n * d_in.element_size() / 1e9
     print(f"compress {tc * 1e3:.1f} us ({gb / tc * 1e3:.0f} GB/s); stages ms: predict {stc[cz.T_PREDICT]:.4f} "
