@@ -24,49 +24,51 @@ namespace {
 
 constexpr int kLmax = 27;
 
-struct HeapNode {
+// 1-based binary min-heap of tree nodes with the reference's tie-breaking (qinsert / qremove,
+// hf_bk_impl1.seq.cc:103-137): a node moves up while its parent is strictly greater, down while
+// the smaller child (the right one only if strictly smaller) is strictly smaller.  Entries carry
+// their frequency, so no comparison goes through the node pool (same order of operations, so
+// the same heap states as the reference's pointer heap).
+struct HeapEntry {
   uint64_t freq;
-  int32_t left;   // -1 for a leaf
-  int32_t right;
-  int32_t symbol;
+  int32_t id;
 };
 
-class MergeHeap {  // 1-based binary min-heap of node ids, reference tie-breaking
+class MergeHeap {
  public:
-  explicit MergeHeap(std::vector<HeapNode>& pool, size_t cap) : pool_(pool), q_(cap + 2, -1) {}
+  explicit MergeHeap(HeapEntry* q) : q_(q) {}
 
-  void push(int32_t id)
+  void push(uint64_t f, int32_t id)
   {
     int i = end_++;
     for (int j = i >> 1; j; j = i >> 1) {
-      if (pool_[q_[j]].freq <= pool_[id].freq) break;
+      if (q_[j].freq <= f) break;
       q_[i] = q_[j];
       i = j;
     }
-    q_[i] = id;
+    q_[i] = {f, id};
   }
 
-  int32_t pop()
+  HeapEntry pop()
   {
-    if (end_ < 2) return -1;
-    const int32_t top = q_[1];
-    q_[1] = q_[--end_];
+    const HeapEntry top = q_[1];
+    const HeapEntry x = q_[--end_];
     int i = 1;
-    for (int l = 2 * i; l < end_; l = 2 * i) {
-      if (l + 1 < end_ && pool_[q_[l + 1]].freq < pool_[q_[l]].freq) l++;
-      if (pool_[q_[i]].freq <= pool_[q_[l]].freq) break;
-      std::swap(q_[i], q_[l]);
+    for (int l = 2; l < end_; l = 2 * i) {
+      if (l + 1 < end_ && q_[l + 1].freq < q_[l].freq) l++;
+      if (x.freq <= q_[l].freq) break;
+      q_[i] = q_[l];
       i = l;
     }
+    q_[i] = x;
     return top;
   }
 
   int size() const { return end_ - 1; }
-  int32_t root() const { return q_[1]; }
+  int32_t root() const { return q_[1].id; }
 
  private:
-  std::vector<HeapNode>& pool_;
-  std::vector<int32_t> q_;
+  HeapEntry* q_;
   int end_ = 1;
 };
 
@@ -106,33 +108,37 @@ int huffman_code_lengths(const uint32_t* hist, int bklen, uint8_t* len)
     len[only] = 1;
     return 1;
   }
-  std::vector<HeapNode> pool;
-  pool.reserve(2 * used);
-  MergeHeap heap(pool, 2 * used);
+  // tree nodes: leaves 0..used-1, internal nodes after them (children ids)
+  thread_local std::vector<int32_t> kid;   // 2 per node
+  thread_local std::vector<int32_t> sym;   // leaf symbol
+  thread_local std::vector<HeapEntry> q;
+  thread_local std::vector<uint8_t> depth;
+  kid.resize(4 * (size_t)used), sym.resize(2 * (size_t)used), q.resize(2 * (size_t)used + 2), depth.resize(2 * (size_t)used);
+  MergeHeap heap(q.data());
+  int32_t nodes = 0;
   for (int s = 0; s < bklen; s++)
     if (hist[s]) {
-      pool.push_back({hist[s], -1, -1, s});
-      heap.push((int32_t)pool.size() - 1);
+      sym[nodes] = s, kid[2 * nodes] = -1;
+      heap.push(hist[s], nodes++);
     }
   while (heap.size() > 1) {
-    const int32_t a = heap.pop(), b = heap.pop();
-    pool.push_back({pool[a].freq + pool[b].freq, a, b, -1});
-    heap.push((int32_t)pool.size() - 1);
+    const HeapEntry a = heap.pop(), b = heap.pop();
+    kid[2 * nodes] = a.id, kid[2 * nodes + 1] = b.id;
+    heap.push(a.freq + b.freq, nodes++);
   }
-  // leaf depths
+  // leaf depths: parents are created after their children, so a reverse sweep from the root
+  // sees every parent before its children
   int deepest = 0;
-  std::vector<std::pair<int32_t, int>> stack{{heap.root(), 0}};
-  while (!stack.empty()) {
-    auto [id, d] = stack.back();
-    stack.pop_back();
-    const HeapNode& nd = pool[id];
-    if (nd.left < 0) {
-      len[nd.symbol] = (uint8_t)std::min(d, 255);
+  depth[nodes - 1] = 0;
+  for (int32_t id = nodes - 1; id >= 0; id--) {
+    const int d = depth[id];
+    if (kid[2 * id] < 0) {
+      len[sym[id]] = (uint8_t)std::min(d, 255);
       deepest = std::max(deepest, d);
     }
     else {
-      stack.push_back({nd.left, d + 1});
-      stack.push_back({nd.right, d + 1});
+      const int dc = std::min(d + 1, 255);
+      depth[kid[2 * id]] = (uint8_t)dc, depth[kid[2 * id + 1]] = (uint8_t)dc;
     }
   }
   if (deepest > kLmax) {
