@@ -555,11 +555,14 @@ k_brick3_pack(const uint16_t* __restrict__ bcodes, uint32_t ly, uint32_t lz, con
 //
 // Steps are grouped in quarters of kF: a lane takes part in a whole quarter or sits it out,
 // decided once from its column count and ring fill (one word crossed per step at most), so the
-// steps carry no predicates.  A lane may thus run up to 2 kF - 1 symbols past the block end,
-// into tile columns [64, 64 + 2 kF], which move to the block's front after the reconstruction.
-// Tile stores are aligned 32-bit pairs (a 2-B aligned 32-bit LDS store stalls the LDS pipeline,
-// SQ_LDS_UNALIGNED_STALL): at an even column the entry's two symbols, at an odd column the symbol
-// kept from the previous step and this step's first.
+// steps carry no predicates.  A step reads one table (L1 or L2, chosen by the window: they are
+// exclusive) and has no branch: a code longer than 16 bits reads entry 0, "no symbol, no bits",
+// so the lane stands still, and one extra step after the quarter decodes it by threshold counting
+// (hf_device.hh lookup_long) for the lanes that need it.  A lane may thus run up to 2 kF + 1
+// symbols past the block end, into tile columns [64, 74), which move to the block's front after
+// the reconstruction.  Tile stores are aligned 32-bit pairs (a 2-B aligned 32-bit LDS store
+// stalls the LDS pipeline, SQ_LDS_UNALIGNED_STALL): at an even column the entry's two symbols,
+// at an odd column the symbol kept from the previous step and this step's first.
 //
 // Outliers.  When the archive's cells are grouped by brick and sorted by (row, x) -- this
 // compressor writes them so, k_brick_cell_bounds checks -- the k-th zero code of a row takes the
@@ -579,7 +582,7 @@ constexpr int kF = CUSZ_AMD_DEC_F;           // decode steps between ring refill
 constexpr int kDecWaves = CUSZ_AMD_DEC_WAVES;  // waves per workgroup (one workgroup per CU)
 constexpr int kBlk = 64;                     // columns reconstructed per block (= lanes)
 constexpr uint32_t kRing = 16;               // ring words per lane (power of two)
-constexpr int kTP = kBlk + 2 + 2 * kF;       // tile row pitch (u16), an odd number of dwords
+constexpr int kTP = kBlk + 6 + 2 * kF;       // tile row pitch (u16), an odd number of dwords
 static_assert(((kTP / 2) & 1) == 1, "odd dword pitch: row r starts at bank (kTP / 2) r");
 constexpr uint32_t kCellCap = 128;           // outlier values of a brick kept in LDS
 // per wave: ring + junk slot | tile | cell values | row starts (65) | row carries (64)
@@ -823,7 +826,7 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
     const uint32_t nbit = live ? par_nbit[c] : 0u;
     const uint32_t vbase = (live ? par_entry[c] : 0u) * 4u;
     const uint32_t nwords = (nbit + 31u) >> 5;
-    // words 0..7 (0..2 into registers, 3..7 into the ring), issued before the cells are read
+    // words 0..7 (0..2 into registers, 2..7 into the ring), issued before the cells are read
     const u32x4 a0 = __builtin_amdgcn_raw_buffer_load_b128(rbits, (int)(live ? vbase : kOOB), 0, 0);
     const u32x4 a1 = __builtin_amdgcn_raw_buffer_load_b128(rbits, (int)(live ? vbase + 16u : kOOB), 0, 0);
     // the brick's outlier cells [cb, ce): per-row counts -> row starts; values into LDS
@@ -849,6 +852,7 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
       bc.vstride = nc <= kCellCap ? 1u : 2u;
     }
     uint32_t w0 = 0, w1 = a0.x, w2 = a0.y, nx = a0.z;
+    ring_lane[2 * 64] = a0.z;  // nx is re-read every step, also by a first step that does not move
     ring_lane[3 * 64] = a0.w;
     ring_lane[4 * 64] = a1.x, ring_lane[5 * 64] = a1.y, ring_lane[6 * 64] = a1.z, ring_lane[7 * 64] = a1.w;
     uint32_t kk = 2;    // word index held by nx
@@ -883,17 +887,23 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
       uint16_t* rowp = tile + lane * kTP - blk * kBlk;  // rowp[cnt] = tile column cnt - 64 blk
       const uint32_t target = (uint32_t)(blk + 1) * kBlk;
       auto quarter = [&]() {
-        BPROF(pc[6] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(cnt < target && !(kk + (uint32_t)kF < rdy)));
-              pc[7] += kF * __builtin_popcountll(__builtin_amdgcn_ballot_w64(cnt < target && kk + (uint32_t)kF < rdy));)
-        if (cnt < target && kk + (uint32_t)kF < rdy) {
-#pragma unroll
-          for (int st = 0; st < kF; st++) {
+        BPROF(pc[6] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(cnt < target && !(kk + (uint32_t)kF + 1u < rdy)));
+              pc[7] += kF * __builtin_popcountll(__builtin_amdgcn_ballot_w64(cnt < target && kk + (uint32_t)kF + 1u < rdy));)
+        if (cnt < target && kk + (uint32_t)kF + 1u < rdy) {  // at most one word crossed per step
+          uint32_t e = 0;
+          auto step = [&](bool lng) {
             const uint32_t win = __builtin_amdgcn_alignbit(w0, w1, sh);  // chunk bits [pos, pos + 32)
-            const uint32_t e = hfd::lookup<kDecB>(tb, rg, win, ubk);
+            // a code longer than 16 bits has no table entry: e = 0 consumes nothing, and the lane
+            // decodes it after the quarter (rare: no branch in the steps)
+#ifdef CUSZ_AMD_TESTA
+            e = hfd::lookup1<kDecB>(tb, rg, win, ubk);
+#else
+            e = lng ? hfd::lookup_long<kDecB>(tb, rg, win, ubk) : hfd::lookup_short<kDecB>(tb, rg, win);
+#endif
             const uint32_t sy = e & hfd::kEntSymMask;
             const bool odd = cnt & 1u;
             *reinterpret_cast<uint32_t*>(rowp + (cnt & ~1u)) = odd ? (keep | (sy << 16)) : sy;
-            keep = odd ? (sy >> 16) : (sy & 0xFFFFu);
+            keep = e == 0 ? keep : (odd ? (sy >> 16) : (sy & 0xFFFFu));
             cnt += hfd::ent_nsym(e);
             const int32_t s2 = (int32_t)sh - (int32_t)hfd::ent_bits(e);
             const bool shf = s2 < 0;  // crossed into the next word
@@ -903,6 +913,11 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
             w2 = shf ? nx : w2;
             kk += shf ? 1u : 0u;
             nx = ring_lane[(kk & (kRing - 1u)) * 64];
+          };
+#pragma unroll
+          for (int st = 0; st < kF; st++) step(false);
+          if (__builtin_amdgcn_ballot_w64(e == 0)) {  // a lane met a long code: one slow step
+            if (e == 0) step(true);
           }
         }
       };
@@ -938,11 +953,11 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
       // symbols decoded past the block end move to its front (`keep` carries a pending one)
       {
         uint32_t* rw = reinterpret_cast<uint32_t*>(tile + lane * kTP);
-        uint32_t v[kF];
+        uint32_t v[kF + 1];
 #pragma unroll
-        for (int i = 0; i < kF; i++) v[i] = rw[kBlk / 2 + i];
+        for (int i = 0; i <= kF; i++) v[i] = rw[kBlk / 2 + i];
 #pragma unroll
-        for (int i = 0; i < kF; i++) rw[i] = v[i];
+        for (int i = 0; i <= kF; i++) rw[i] = v[i];
       }
       hfd::wave_sync();
       BPROF(tk = __builtin_readcyclecounter(); pc[4] += tk - tp; tp = tk;)

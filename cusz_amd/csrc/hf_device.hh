@@ -7,6 +7,8 @@
 // first[l]].  revbook layout (hf_bk.seq.cc:135-142): first i32[32] | entry i32[32] | keys[bklen].
 #pragma once
 
+#include <cstddef>
+
 #include "common.hh"
 
 namespace cusz_amd {
@@ -92,15 +94,17 @@ __device__ __forceinline__ void pack4_or(uint32_t* cells, uint32_t pos, const ui
 }
 
 // ---- decode tables --------------------------------------------------------------------------
-// Entry (u32) for the codeword(s) at the top of a window: [9:0] first symbol, [25:16] second
-// symbol, [30:26] bits consumed, [31] two symbols.  0 = not in this table.  The symbols sit
-// where one 32-bit LDS store writes them as two consecutive u16 codes (value & 0x03FF03FF).
+// Entry (u32) for the codeword(s) at the top of a window: [9:0] first symbol, [15:14] symbols
+// (1 or 2), [25:16] second symbol, [30:26] bits consumed, [31] two symbols.  0 = not in this
+// table -- and, read as an entry, "0 symbols, 0 bits": a decoder may step on it without moving.
+// The symbols sit where one 32-bit LDS store writes them as two consecutive u16 codes
+// (value & 0x03FF03FF).
 __device__ __forceinline__ uint32_t ent_pack(uint32_t two, uint32_t bits, uint32_t s0, uint32_t s1)
 {
-  return (two << 31) | (bits << 26) | (s1 << 16) | s0;
+  return (two << 31) | (bits << 26) | (s1 << 16) | ((1u + two) << 14) | s0;
 }
 __device__ __forceinline__ uint32_t ent_bits(uint32_t e) { return (e >> 26) & 31u; }
-__device__ __forceinline__ uint32_t ent_nsym(uint32_t e) { return 1u + (e >> 31); }
+__device__ __forceinline__ uint32_t ent_nsym(uint32_t e) { return (e >> 14) & 3u; }
 constexpr uint32_t kEntSymMask = 0x03FF03FFu;
 
 // longest code length present (last l with entry[l+1] > entry[l])
@@ -162,6 +166,7 @@ constexpr int kSlowFrom = 12;
 struct DecRegs {
   uint32_t first[kLmax - kSlowFrom + 1];
   uint32_t maxl;
+  uint32_t thr;  // windows below thr start with a code longer than B bits (lookup1)
 };
 
 // Cooperative build by the whole workgroup (ends with a barrier).
@@ -218,6 +223,9 @@ __device__ __forceinline__ DecRegs load_dec_regs(const LdsTables<B>& t)
 #pragma unroll
   for (int q = 0; q < kLmax - kSlowFrom + 1; q++) r.first[q] = __builtin_amdgcn_readfirstlane(t.first[kSlowFrom + q]);
   r.maxl = __builtin_amdgcn_readfirstlane(t.maxl);
+  // canonical codes: a code is longer than B bits iff the window's top B bits are < first[B]
+  const uint32_t fb = __builtin_amdgcn_readfirstlane(t.first[B]);
+  r.thr = r.maxl <= (uint32_t)B ? 0u : (fb >= (1u << B) ? 0xFFFFFFFFu : fb << (32 - B));
   return r;
 }
 
@@ -231,6 +239,49 @@ __device__ __forceinline__ uint32_t lookup(const LdsTables<B>& t, const DecRegs&
   if (__builtin_expect(e == 0, 0)) {  // all lengths <= 16 failed: count the rest
     uint32_t l = B + 1;
 #pragma unroll CUSZ_AMD_SLOW_UNROLL
+    for (int q = B + 1 - kSlowFrom; q < kLmax - kSlowFrom + 1; q++)
+      l += (kSlowFrom + q < (int)rg.maxl && (win >> (32 - (kSlowFrom + q))) < rg.first[q]) ? 1u : 0u;
+    if (l > rg.maxl) l = rg.maxl;
+    const uint32_t s = t.keys[min(t.base[l] + (win >> (32 - l)), bklen - 1)];
+    e = ent_pack(0, l, s, 0);
+  }
+  return e;
+}
+
+// The rare codes longer than 16 bits (no table entry): count the failing lengths against the
+// thresholds in registers.
+template <int B>
+__device__ __forceinline__ uint32_t lookup_long(const LdsTables<B>& t, const DecRegs& rg, uint32_t win, uint32_t bklen)
+{
+  uint32_t l = B + 1;
+#pragma unroll
+  for (int q = B + 1 - kSlowFrom; q < kLmax - kSlowFrom + 1; q++)
+    l += (kSlowFrom + q < (int)rg.maxl && (win >> (32 - (kSlowFrom + q))) < rg.first[q]) ? 1u : 0u;
+  if (l > rg.maxl) l = rg.maxl;
+  const uint32_t s = t.keys[min(t.base[l] + (win >> (32 - l)), bklen - 1)];
+  return ent_pack(0, l, s, 0);
+}
+
+// One table read, no branch: the entry, or 0 for a code longer than 16 bits (lookup_long).
+template <int B>
+__device__ __forceinline__ uint32_t lookup_short(const LdsTables<B>& t, const DecRegs& rg, uint32_t win)
+{
+  const uint32_t a = win < rg.thr ? (1u << B) + min(win >> (32 - kL2Bits), (uint32_t)kL2Cap - 1) : win >> (32 - B);
+  return t.l1[a];
+}
+
+// Same entry as lookup() with ONE table read: L1 and L2 are exclusive (L2 holds exactly the
+// windows below rg.thr), so the window picks its table before the read.  L2 follows L1 in
+// LdsTables, so both are one array.
+template <int B>
+__device__ __forceinline__ uint32_t lookup1(const LdsTables<B>& t, const DecRegs& rg, uint32_t win, uint32_t bklen)
+{
+  static_assert(offsetof(LdsTables<B>, l2) == sizeof(uint32_t) << B, "l2 follows l1");
+  const uint32_t a = win < rg.thr ? (1u << B) + min(win >> (32 - kL2Bits), (uint32_t)kL2Cap - 1) : win >> (32 - B);
+  uint32_t e = t.l1[a];
+  if (__builtin_expect(e == 0, 0)) {  // all lengths <= 16 failed: count the rest
+    uint32_t l = B + 1;
+#pragma unroll
     for (int q = B + 1 - kSlowFrom; q < kLmax - kSlowFrom + 1; q++)
       l += (kSlowFrom + q < (int)rg.maxl && (win >> (32 - (kSlowFrom + q))) < rg.first[q]) ? 1u : 0u;
     if (l > rg.maxl) l = rg.maxl;
