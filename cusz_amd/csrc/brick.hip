@@ -728,19 +728,47 @@ __device__ __forceinline__ void recon_block(const uint16_t* tile, T* out, size_t
         if (cd[z] == 0u) v[z] = ZZ ? ov[z] + T(0) : ov[z] - r;
     }
     T t[8];
+    if constexpr (sizeof(T) == 4) {
+      // the same IEEE operations, two z rows per packed instruction where the operands pair up
+      // (v_pk_add_f32 / v_pk_mul_f32): the y sums, the z Hillis-Steele steps d = 2, 4, the scale
+      typedef float f2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-    for (int z = 0; z < 8; z++) {
-      s[z] = y > 0 ? s[z] + v[z] : v[z];
-      t[z] = x_scan8<T>(s[z], l7);
+      for (int j = 0; j < 4; j++) {
+        f2 sv = {s[2 * j], s[2 * j + 1]};
+        const f2 vv = {v[2 * j], v[2 * j + 1]};
+        sv = y > 0 ? sv + vv : vv;
+        s[2 * j] = sv.x, s[2 * j + 1] = sv.y;
+        t[2 * j] = x_scan8<T>(sv.x, l7), t[2 * j + 1] = x_scan8<T>(sv.y, l7);
+      }
+#pragma unroll
+      for (int z = 7; z >= 1; z--) t[z] = t[z] + t[z - 1];
+      f2 tp[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) tp[j] = f2{t[2 * j], t[2 * j + 1]};
+      tp[3] = tp[3] + tp[2], tp[2] = tp[2] + tp[1], tp[1] = tp[1] + tp[0];  // d = 2 (descending)
+      tp[3] = tp[3] + tp[1], tp[2] = tp[2] + tp[0];                          // d = 4
+#pragma unroll
+      for (int j = 0; j < 4; j++) tp[j] = tp[j] * f2{(float)ebx2, (float)ebx2};
+#pragma unroll
+      for (int j = 0; j < 4; j++) t[2 * j] = tp[j].x, t[2 * j + 1] = tp[j].y;
     }
+    else {
 #pragma unroll
-    for (int d = 1; d < 8; d *= 2)
+      for (int z = 0; z < 8; z++) {
+        s[z] = y > 0 ? s[z] + v[z] : v[z];
+        t[z] = x_scan8<T>(s[z], l7);
+      }
 #pragma unroll
-      for (int z = 7; z >= d; z--) t[z] = t[z] + t[z - d];
+      for (int d = 1; d < 8; d *= 2)
+#pragma unroll
+        for (int z = 7; z >= d; z--) t[z] = t[z] + t[z - d];
+#pragma unroll
+      for (int z = 0; z < 8; z++) t[z] = t[z] * ebx2;
+    }
 #pragma unroll
     for (int z = 0; z < 8; z++) {
       if ((uint32_t)z >= nzv) break;
-      const T o = t[z] * ebx2;
+      const T o = t[z];
       if constexpr (BUF)
         buf_store<T>(o, ro, voff, (uint32_t)(((size_t)z * plane + (size_t)y * lx) * sizeof(T)));
       else
