@@ -193,7 +193,7 @@ constexpr int kScanAhead = sizeof(T) == 4 ? CUSZ_AMD_SCAN_AHEAD : 8;
 template <typename T, int V, bool ZZ>
 __global__ void __launch_bounds__(64 * kBrickWaves)
 k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T ebx2_r, T r, OutlierSink ol,
-              uint32_t* __restrict__ g_hist, uint16_t* __restrict__ bhist, uint16_t* __restrict__ bcodes, int bklen,
+              uint32_t* __restrict__ g_hist, uint16_t* __restrict__ bhist, BrickCodes bcs, int bklen,
               uint32_t nbx, uint32_t nby, uint32_t nbricks)
 {
   extern __shared__ uint32_t smem[];
@@ -215,6 +215,8 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
   T q[D][V];
 #pragma unroll
   for (int j = 0; j < D; j++) ld.issue_row(u * kUnitBricks, j, q[j]);
+  static_assert(kUnitBricks == 1, "one row mask per unit");
+  uint64_t rowmask = 0;  // rows of the brick stored as u16 (uniform)
   for (; u < nunits; u += nw) {
     uint32_t cnt = 0;
     const uint32_t bend = min((u + 1) * kUnitBricks, nbricks);
@@ -222,7 +224,9 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
       const uint32_t bnext = brick + 1 < bend ? brick + 1 : (u + nw) * kUnitBricks;  // next brick of the stream
       const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
       const uint32_t x0 = bx * (64 * V) + lane * V, y0 = by * 8, z0 = bz * 8;
-      uint16_t* cbrick = bcodes + (size_t)brick * 64 * (64 * V) + (size_t)lane * V;
+      uint16_t* cbrick = bcs.c16 + (size_t)brick * 64 * (64 * V) + (size_t)lane * V;
+      uint8_t* cbrick8 = bcs.c8 + (size_t)brick * 64 * (64 * V) + (size_t)lane * V;
+      rowmask = 0;
       T bprev[8][V], pprev[V];
 #pragma unroll 1
       for (int r0 = 0; r0 < 64; r0 += D)  // not unrolled: instruction cache
@@ -266,7 +270,22 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
 #endif
           }
 #ifndef CUSZ_AMD_SCAN_NOCODES  // (timing experiment switch: no code stores)
-          store_codes_row<V>(cbrick + (size_t)row * (64 * V), qc);
+          {
+            static_assert(V == 4, "one 4-B byte-code store per lane and row");
+            bool wide = false;
+#pragma unroll
+            for (int k = 0; k < V; k++) wide |= (uint32_t)qc[k] - bcs.c0 > 254u;
+            if (__builtin_amdgcn_ballot_w64(wide)) {
+              store_codes_row<V>(cbrick + (size_t)row * (64 * V), qc);
+              rowmask |= 1ull << row;
+            }
+            else {
+              uint32_t w = 0;
+#pragma unroll
+              for (int k = 0; k < V; k++) w |= ((uint32_t)qc[k] - bcs.c0) << (8 * k);
+              *reinterpret_cast<uint32_t*>(cbrick8 + (size_t)row * (64 * V)) = w;
+            }
+          }
 #endif
           if (anyol) {
             uint32_t mask = 0;
@@ -282,6 +301,7 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
         }
     }
     if (lane == 0) ol.brick_cnt[u] = cnt;
+    if (lane == 0) bcs.rowmask[u] = rowmask;  // kUnitBricks == 1: unit = brick
     hfd::wave_sync();
     // unit histogram -> u16 record (16-B stores, 8 bins per lane) and the workgroup histogram
     uint16_t* bh = bhist + (size_t)u * hs;
@@ -437,7 +457,7 @@ constexpr int pack_cells_words()
 // The codes of the next y-step are loaded while the current one is packed.
 template <int V>
 __global__ void __launch_bounds__(64 * kBrickWaves)
-k_brick3_pack(const uint16_t* __restrict__ bcodes, uint32_t ly, uint32_t lz, const uint32_t* __restrict__ book,
+k_brick3_pack(BrickCodes bcs, uint32_t ly, uint32_t lz, const uint32_t* __restrict__ book,
               int bklen, BrickPlanArgs pl, uint32_t* __restrict__ par_nbit, uint32_t* __restrict__ par_entry,
               uint32_t* __restrict__ bitstream, uint32_t nbx, uint32_t nby, uint32_t nbricks, int reverse,
               unsigned int* overflow)
@@ -482,21 +502,39 @@ k_brick3_pack(const uint16_t* __restrict__ bcodes, uint32_t ly, uint32_t lz, con
       const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
       const uint32_t y0 = by * 8, z0 = bz * 8;
       const uint32_t nyv = min(8u, ly - y0), nzv = min(8u, lz - z0);
-      const uint2* src = reinterpret_cast<const uint2*>(bcodes + (size_t)brick * 64 * (64 * V)) + lane;
+      const uint8_t* src16 = reinterpret_cast<const uint8_t*>(bcs.c16 + (size_t)brick * 64 * (64 * V)) + lane * 8;
+      const uint8_t* src8 = bcs.c8 + (size_t)brick * 64 * (64 * V) + lane * 4;
+      const uint64_t rm = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bcs.rowmask[brick]) & 0xFFFFFFFFull) |
+                          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(bcs.rowmask[brick] >> 32)) << 32);
+      // row r: 8 u16 bytes per lane when bit r of rm is set, else 4 code bytes (.x); one 8-B load
+      // either way (a byte row's lane reads its neighbour's 4 bytes too: no branch around loads)
+      auto load_row = [&](uint32_t row) -> uint2 {
+        const uint8_t* a = (rm >> row) & 1ull ? src16 + (size_t)row * 512 : src8 + (size_t)row * 256;
+        uint2 v;
+        __builtin_memcpy(&v, a, 8);
+        return v;
+      };
       uint32_t my_nbit = 0, my_entry = 0;
       uint2 cur[8], nxt[8];
 #pragma unroll
-      for (int z = 0; z < 8; z++) nxt[z] = (uint32_t)z < nzv ? src[z * 64] : make_uint2(0, 0);
+      for (int z = 0; z < 8; z++) nxt[z] = (uint32_t)z < nzv ? load_row(z) : make_uint2(0, 0);
       for (uint32_t y = 0; y < nyv; y++) {
 #pragma unroll
         for (int z = 0; z < 8; z++) cur[z] = nxt[z];
         if (y + 1 < nyv)
 #pragma unroll
-          for (int z = 0; z < 8; z++) nxt[z] = (uint32_t)z < nzv ? src[((y + 1) * 8 + z) * 64] : make_uint2(0, 0);
+          for (int z = 0; z < 8; z++) nxt[z] = (uint32_t)z < nzv ? load_row((y + 1) * 8 + z) : make_uint2(0, 0);
 #pragma unroll
         for (int z = 0; z < 8; z++) {
           if ((uint32_t)z >= nzv) break;
-          const uint32_t qs[4] = {cur[z].x & 0xFFFFu, cur[z].x >> 16, cur[z].y & 0xFFFFu, cur[z].y >> 16};
+          uint32_t qs[4];
+          if ((rm >> (y * 8 + z)) & 1ull) {
+            qs[0] = cur[z].x & 0xFFFFu, qs[1] = cur[z].x >> 16, qs[2] = cur[z].y & 0xFFFFu, qs[3] = cur[z].y >> 16;
+          }
+          else {
+#pragma unroll
+            for (int k = 0; k < 4; k++) qs[k] = ((cur[z].x >> (8 * k)) & 255u) + bcs.c0;
+          }
           uint32_t w[V], bits = 0;
 #pragma unroll
           for (int k = 0; k < V; k++) {
@@ -1048,7 +1086,7 @@ int brick_configure(BrickLaunch& L, int elem_bytes, int device)
 
 template <typename T>
 int launch_brick_scan(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const OutlierSink& ol,
-                      uint32_t* hist, uint16_t* bhist, uint16_t* bcodes, int bklen, hipStream_t st)
+                      uint32_t* hist, uint16_t* bhist, const BrickCodes& bcodes, int bklen, hipStream_t st)
 {
   const T ebx2_r = (T)(1.0 / (eb * 2));  // lrz_c.cuhip.inl:489
   const T r = (T)radius;
@@ -1078,7 +1116,7 @@ uint32_t brick_units(uint32_t nbricks) { return (nbricks + kUnitBricks - 1) / kU
 uint32_t brick_plan_blocks(uint32_t nbricks) { return (brick_units(nbricks) + kPlanBricks - 1) / kPlanBricks; }
 int brick_hist_stride(int bklen) { return bhist_stride(bklen); }
 
-int launch_brick_pack(const BrickLaunch& L, const uint16_t* bcodes, const uint32_t* book, int bklen,
+int launch_brick_pack(const BrickLaunch& L, const BrickCodes& bcodes, const uint32_t* book, int bklen,
                       const BrickPlanArgs& plan, uint32_t* par_nbit, uint32_t* par_entry, uint32_t* bitstream,
                       int reverse, unsigned int* overflow, hipStream_t st)
 {
@@ -1143,7 +1181,7 @@ extern "C" int psz_amd_debug_brick_profile(unsigned long long* host, int reset)
 
 #define INST(T)                                                                                                   \
   template int launch_brick_scan<T>(const BrickLaunch&, const T*, double, int, bool, const OutlierSink&, uint32_t*, \
-                                    uint16_t*, uint16_t*, int, hipStream_t);                                       \
+                                    uint16_t*, const BrickCodes&, int, hipStream_t);                               \
   template int launch_brick_decode<T>(const BrickLaunch&, const uint32_t*, size_t, const uint8_t*, int,            \
                                       const uint32_t*, const uint32_t*, T*, double, int, bool, const BrickOutliers&, \
                                       hipStream_t);

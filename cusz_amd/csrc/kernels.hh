@@ -202,11 +202,20 @@ struct BrickLaunch {
 // fills ncu and the encode-pass grids for `device`
 int brick_configure(BrickLaunch& L, int elem_bytes, int device);
 
-// pass 1: predict -> global + per-brick histograms, outliers, codes in brick order (bcodes:
-// nbricks * 64 rows * W u16)
+// Quant codes between the two encode passes, in brick order (row r of brick b at (64 b + r) W).
+// A row whose codes all lie in [c0, c0 + 254] is stored as bytes (code - c0) in c8; any other
+// row as u16 codes in c16, with bit r of rowmask[b] set.  c0 = radius - 127 (ZigZag: 0): the
+// rows that are not u16 are about 90 % of a smooth field's (those off the tiles' first z plane).
+struct BrickCodes {
+  uint16_t* c16;      // nbricks * 64 * W u16 (written only for the u16 rows)
+  uint8_t* c8;        // nbricks * 64 * W bytes
+  uint64_t* rowmask;  // nbricks
+  uint32_t c0;
+};
+// pass 1: predict -> global + per-brick histograms, outliers, codes in brick order
 template <typename T>
 int launch_brick_scan(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const OutlierSink& ol,
-                      uint32_t* hist, uint16_t* bhist, uint16_t* bcodes, int bklen, hipStream_t st);
+                      uint32_t* hist, uint16_t* bhist, const BrickCodes& bc, int bklen, hipStream_t st);
 // archive plan (brick.hip k_brick_plan): region sizes, cell / outlier offsets, totals, headers
 struct BrickPlanArgs {
   const uint16_t* bhist;  // per-brick histograms, stride brick_hist_stride(bklen)
@@ -235,7 +244,7 @@ int brick_hist_stride(int bklen);
 int launch_brick_plan(const BrickLaunch& L, const BrickPlanArgs& a, const void* psz_tpl, const void* phf_tpl,
                       hipStream_t st);
 // pass 2: brick-ordered codes -> Huffman cells at each brick's reserved region
-int launch_brick_pack(const BrickLaunch& L, const uint16_t* bcodes, const uint32_t* book, int bklen,
+int launch_brick_pack(const BrickLaunch& L, const BrickCodes& bc, const uint32_t* book, int bklen,
                       const BrickPlanArgs& plan, uint32_t* par_nbit, uint32_t* par_entry, uint32_t* bitstream,
                       int reverse, unsigned int* overflow, hipStream_t st);
 // Outlier cells for the fused decoder: when the archive's cells are grouped by brick and sorted

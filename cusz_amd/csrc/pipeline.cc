@@ -103,6 +103,8 @@ struct Pipeline {
 
   // device
   uint16_t* d_codes = nullptr;
+  uint8_t* d_codes8 = nullptr;     // brick layout: byte rows between the encode passes
+  uint64_t* d_rowmask = nullptr;   // brick layout: u16 rows per brick
   uint32_t* d_hist = nullptr;
   uint32_t* d_book = nullptr;
   uint64_t* d_slots = nullptr;
@@ -147,7 +149,8 @@ struct Pipeline {
     for (void* p : {(void*)d_codes, (void*)d_hist, (void*)d_book, (void*)d_slots, (void*)d_brick_cnt,
                     (void*)d_brick_off, (void*)d_spill, (void*)d_small, (void*)d_status, (void*)d_archive,
                     (void*)d_enc_temp, (void*)d_spl_slots, (void*)d_spl_cnt, (void*)d_spl_off, (void*)d_spl_x, (void*)d_spl_sps,
-                    (void*)d_bhist, (void*)d_ub, (void*)d_bbase, (void*)d_plan, (void*)d_x1d})
+                    (void*)d_bhist, (void*)d_ub, (void*)d_bbase, (void*)d_plan, (void*)d_x1d, (void*)d_codes8,
+                    (void*)d_rowmask})
       if (p) (void)hipFree(p);
     if (h_xfer) (void)hipHostFree(h_xfer);
     for (auto& e : ev)
@@ -156,6 +159,7 @@ struct Pipeline {
     d_brick_off = nullptr, d_spill = nullptr, d_small = nullptr, d_status = nullptr, d_archive = nullptr;
     d_enc_temp = nullptr;
     d_bhist = nullptr, d_ub = nullptr, d_bbase = nullptr, d_plan = nullptr, d_x1d = nullptr;
+    d_codes8 = nullptr, d_rowmask = nullptr;
     d_spl_slots = nullptr, d_spl_cnt = nullptr, d_spl_off = nullptr, d_spl_x = nullptr, d_spl_sps = nullptr;
     spl_slot_cells = 0, spl_x_words = 0;
     h_xfer = nullptr;
@@ -212,6 +216,8 @@ struct Pipeline {
       CUSZ_AMD_HIP_CHECK(hipMalloc(&d_plan, 2 * ((size_t)brick_plan_blocks(bl.g.nbricks) + 1) * 4));
       // fused decompression: per-brick first outlier cell + unsorted flag (d_x1d's role in 1-D)
       if (!d_x1d) CUSZ_AMD_HIP_CHECK(hipMalloc(&d_x1d, ((size_t)bl.g.nbricks + 2) * 4));
+      CUSZ_AMD_HIP_CHECK(hipMalloc(&d_codes8, (size_t)bl.g.nbricks * bl.g.brick_elems + 64));  // + 8-B load slack
+      CUSZ_AMD_HIP_CHECK(hipMalloc(&d_rowmask, (size_t)bl.g.nbricks * 8));
     }
 
     // codes: index order (reference layout) or brick order (brick layout: whole bricks)
@@ -298,7 +304,7 @@ struct Pipeline {
 
   // state carried from compress_scan (pass 1) to compress_finish (codebook onwards)
   struct Pending {
-    bool active = false, brick = false, spl = false;
+    bool active = false, brick = false, spl = false, zz = false;
     int radius = 0;
     size_t anchor_bytes = 0;
   } pend;
@@ -366,12 +372,12 @@ struct Pipeline {
                                                  stream));
     mark(1);
     last_layout = brick ? PSZ_AMD_LAYOUT_BRICK : PSZ_AMD_LAYOUT_REFERENCE;
-    pend.brick = brick, pend.spl = spl, pend.radius = radius;
+    pend.brick = brick, pend.spl = spl, pend.radius = radius, pend.zz = zz;
     pend.anchor_bytes = spl ? sizeof(T) * sgeom.anchor_len : 0;
     if (brick) {
       OutlierSink bol{d_slots, d_brick_cnt, d_spill, spill_cnt(), brick_cap(), spill_cap, nullptr};
-      CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_scan<T>(bl, in, eb, radius, zz, bol, d_hist, d_bhist, d_codes,
-                                                          bklen, stream));
+      CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_scan<T>(bl, in, eb, radius, zz, bol, d_hist, d_bhist,
+                                                          brick_codes(zz, radius), bklen, stream));
       mark(2);
       pend.active = true;
       return PSZ_SUCCESS;
@@ -482,6 +488,11 @@ struct Pipeline {
 
   // Fused brick compress (brick.hip): pass 1 (histograms + outliers) -> host codebook ->
   // region reservation -> pass 2 (predict + pack straight into the archive) -> finalize.
+  BrickCodes brick_codes(bool zz, int radius) const
+  {
+    return BrickCodes{d_codes, d_codes8, d_rowmask, zz ? 0u : (uint32_t)std::max(radius - 127, 0)};
+  }
+
   int compress_brick(psz_header* h, uint8_t** out, size_t* outlen, int radius)
   {
     const int bklen = 2 * radius;
@@ -546,7 +557,7 @@ struct Pipeline {
                      d_brick_cnt, cap, d_slots, d_spill, spill_cnt(), spill_cap, nblk, d_ub, d_bbase, d_brick_off,
                      d_plan, d_plan + nblk + 1, info(), d_archive, phf_off, bits_rel};
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_plan(bl, pa, h, &ph, stream));
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_pack(bl, d_codes, d_book, bklen, pa, par_nbit, par_entry, bits,
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_pack(bl, brick_codes(pend.zz, radius), d_book, bklen, pa, par_nbit, par_entry, bits,
                                                      pack_reverse, timeout(), stream));
     mark(4);
     if (gated)
