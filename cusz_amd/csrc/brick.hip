@@ -828,12 +828,12 @@ __device__ unsigned long long g_brick_prof[16];
 
 // Cells of a brick-layout archive: bstart[b] = first cell of brick b (nbricks + 1 entries) and
 // *unsorted != 0 unless the cells are grouped by brick and sorted by (row, x) inside each brick
-// -- key (brick, row = (y % 8) * 8 + z % 8, x % 256) strictly increasing.  bstart and *unsorted
-// are zeroed before the launch.
+// -- key (brick, row = (y % 8) * 8 + z % 8, x % 256) strictly increasing: then every bstart
+// entry is written; otherwise *unsorted = epoch (the word is never reset: no memset launch).
 __global__ void __launch_bounds__(256) k_brick_cell_bounds(const uint32_t* __restrict__ cells, size_t ncell,
                                                            uint32_t lx, uint32_t ly, uint32_t lz, uint32_t nbx,
                                                            uint32_t nby, uint32_t nbricks, uint32_t* bstart,
-                                                           uint32_t* unsorted)
+                                                           uint32_t* unsorted, uint32_t epoch)
 {
   auto key = [&](uint32_t idx, uint32_t& brick) -> uint64_t {
     const uint32_t x = idx % lx, yz = idx / lx, y = yz % ly, z = yz / ly;
@@ -846,10 +846,10 @@ __global__ void __launch_bounds__(256) k_brick_cell_bounds(const uint32_t* __res
     int64_t prev = -1;
     if (i > 0) {
       const uint64_t kp = key(cells[2 * i - 1], bp);
-      if (kp >= k) atomicOr(unsorted, 1u);
+      if (kp >= k) *unsorted = epoch;
       prev = bp;
     }
-    if (b >= nbricks) atomicOr(unsorted, 1u);
+    if (b >= nbricks) *unsorted = epoch;
     for (int64_t u = prev + 1; u <= (int64_t)b && u <= (int64_t)nbricks; u++) bstart[u] = (uint32_t)i;
     if (i + 1 == ncell)
       for (int64_t u = (int64_t)b + 1; u <= (int64_t)nbricks; u++) bstart[u] = (uint32_t)ncell;
@@ -873,7 +873,7 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
   uint16_t* tile = reinterpret_cast<uint16_t*>(wbase + kDecTile);
   uint32_t* cval = reinterpret_cast<uint32_t*>(wbase + kDecCells);
   BrickCells bc{cval, 1, reinterpret_cast<uint32_t*>(wbase + kDecRows), reinterpret_cast<uint32_t*>(wbase + kDecRows) + 65};
-  const bool ranked = !ZZ && (ol.ncell == 0 || !*ol.unsorted);
+  const bool ranked = !ZZ && (ol.ncell == 0 || *ol.unsorted != ol.epoch);
   const __amdgpu_buffer_rsrc_t rbits =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(bitstream), 0, (int)(bs_words * 4u), (int)kBufRsrcW3);
   const size_t plane = (size_t)lx * ly;
@@ -1129,12 +1129,12 @@ int launch_brick_pack(const BrickLaunch& L, const BrickCodes& bcodes, const uint
 }
 
 int launch_brick_cell_bounds(const BrickLaunch& L, const uint32_t* cells, size_t ncell, uint32_t* bstart,
-                             uint32_t* unsorted, hipStream_t st)
+                             uint32_t* unsorted, uint32_t epoch, hipStream_t st)
 {
   if (!ncell) return (int)hipSuccess;
   const uint32_t grid = (uint32_t)std::min<size_t>((ncell + 255) / 256, 2048);
   k_brick_cell_bounds<<<grid, 256, 0, st>>>(cells, ncell, L.lx, L.ly, L.lz, L.g.nbx, L.g.nby, L.g.nbricks, bstart,
-                                            unsorted);
+                                            unsorted, epoch);
   return (int)hipGetLastError();
 }
 

@@ -30,10 +30,11 @@ struct X1dOutliers {
   const uint32_t* cells = nullptr;
   size_t ncell = 0;
   const uint32_t* bstart = nullptr;
-  const uint32_t* unsorted = nullptr;
+  const uint32_t* unsorted = nullptr;  // == epoch: unsorted (the flag word is never reset)
+  uint32_t epoch = 0;
 };
 int launch_x1d_bounds(const uint32_t* cells, size_t ncell, size_t n, uint32_t nbricks, uint32_t* bstart,
-                      uint32_t* unsorted, hipStream_t st);
+                      uint32_t* unsorted, uint32_t epoch, hipStream_t st);
 
 template <typename T>
 int launch_lorenzo_x(const uint16_t* codes, T* out, size_t lx, size_t ly, size_t lz, double eb, int radius,
@@ -41,7 +42,7 @@ int launch_lorenzo_x(const uint16_t* codes, T* out, size_t lx, size_t ly, size_t
 
 template <typename T>
 int launch_scatter(const uint32_t* cells, size_t nnz, T* out, size_t n, hipStream_t st,
-                   const uint32_t* only_if = nullptr);
+                   const uint32_t* only_if = nullptr, uint32_t epoch = 0);
 
 // ---- Huffman (huffman.hip) ---------------------------------------------------------------
 struct HfEncodeArgs {
@@ -255,10 +256,11 @@ struct BrickOutliers {
   const uint32_t* cells = nullptr;  // archive cells {f32 value, u32 idx}
   size_t ncell = 0;
   const uint32_t* bstart = nullptr;   // nbricks + 1
-  const uint32_t* unsorted = nullptr;
+  const uint32_t* unsorted = nullptr;  // == epoch: unsorted (the flag word is never reset)
+  uint32_t epoch = 0;
 };
 int launch_brick_cell_bounds(const BrickLaunch& L, const uint32_t* cells, size_t ncell, uint32_t* bstart,
-                             uint32_t* unsorted, hipStream_t st);
+                             uint32_t* unsorted, uint32_t epoch, hipStream_t st);
 template <typename T>
 int launch_brick_decode(const BrickLaunch& L, const uint32_t* bitstream, size_t bs_words, const uint8_t* revbook,
                         int bklen, const uint32_t* par_nbit, const uint32_t* par_entry, T* out, double eb, int radius,

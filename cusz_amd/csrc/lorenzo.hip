@@ -258,7 +258,7 @@ k_lorenzo_x1d(const uint16_t* __restrict__ codes, T* out, size_t n, T ebx2, T r,
   const int lane = threadIdx.x & 63;
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
   // outlier values from the sorted cells (see X1dOutliers) instead of the scattered `out`
-  const bool fused = !ZZ && ox.cells && !*ox.unsorted;
+  const bool fused = !ZZ && ox.cells && *ox.unsorted != ox.epoch;
   const uint64_t lt = (1ull << lane) - 1;
   for (uint32_t brick = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); brick < nbricks; brick += nw) {
     const size_t bbase = (size_t)brick * 16384;
@@ -482,9 +482,9 @@ k_lorenzo_x3d(const uint16_t* __restrict__ codes, T* out, uint32_t lx, uint32_t 
 // the archive (read as two u32).
 template <typename T>
 __global__ void __launch_bounds__(256)
-k_scatter(const uint32_t* __restrict__ cells, size_t nnz, T* out, size_t n, const uint32_t* only_if)
+k_scatter(const uint32_t* __restrict__ cells, size_t nnz, T* out, size_t n, const uint32_t* only_if, uint32_t epoch)
 {
-  if (only_if && !*only_if) return;  // the 1-D reconstruction reads the sorted cells itself
+  if (only_if && *only_if != epoch) return;  // the 1-D reconstruction reads the sorted cells itself
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nnz; i += (size_t)gridDim.x * blockDim.x) {
     const uint32_t vb = cells[2 * i], idx = cells[2 * i + 1];
     if (idx < n) out[idx] = (T)__builtin_bit_cast(float, vb);
@@ -492,9 +492,10 @@ k_scatter(const uint32_t* __restrict__ cells, size_t nnz, T* out, size_t n, cons
 }
 
 // first cell of every 1-D brick (16384 elements) and whether the cells are strictly increasing
-// (bstart and *unsorted zeroed before)
+// (every bstart entry is written when the cells are sorted; *unsorted = epoch otherwise)
 __global__ void __launch_bounds__(256) k_x1d_bounds(const uint32_t* __restrict__ cells, size_t ncell, size_t n,
-                                                    uint32_t nbricks, uint32_t* bstart, uint32_t* unsorted)
+                                                    uint32_t nbricks, uint32_t* bstart, uint32_t* unsorted,
+                                                    uint32_t epoch)
 {
   for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < ncell; i += (size_t)gridDim.x * 256) {
     const uint32_t idx = cells[2 * i + 1];
@@ -502,10 +503,10 @@ __global__ void __launch_bounds__(256) k_x1d_bounds(const uint32_t* __restrict__
     int64_t bp = -1;
     if (i > 0) {
       const uint32_t ip = cells[2 * i - 1];
-      if (ip >= idx) atomicOr(unsorted, 1u);
+      if (ip >= idx) *unsorted = epoch;
       bp = ip < n ? (int64_t)(ip / 16384) : (int64_t)nbricks;
     }
-    if (idx >= n) atomicOr(unsorted, 1u);
+    if (idx >= n) *unsorted = epoch;
     for (int64_t u = bp + 1; u <= b && u <= (int64_t)nbricks; u++) bstart[u] = (uint32_t)i;
     if (i + 1 == ncell)
       for (int64_t u = b + 1; u <= (int64_t)nbricks; u++) bstart[u] = (uint32_t)ncell;
@@ -614,22 +615,23 @@ int launch_lorenzo_x(const uint16_t* codes, T* out, size_t lx, size_t ly, size_t
 }
 
 template <typename T>
-int launch_scatter(const uint32_t* cells, size_t nnz, T* out, size_t n, hipStream_t st, const uint32_t* only_if)
+int launch_scatter(const uint32_t* cells, size_t nnz, T* out, size_t n, hipStream_t st, const uint32_t* only_if,
+                   uint32_t epoch)
 {
   if (nnz == 0) return 0;
   uint32_t grid = cdiv(nnz, 256);
   if (grid > 4096) grid = 4096;
-  k_scatter<T><<<grid, 256, 0, st>>>(cells, nnz, out, n, only_if);
+  k_scatter<T><<<grid, 256, 0, st>>>(cells, nnz, out, n, only_if, epoch);
   return (int)hipGetLastError();
 }
 
 int launch_x1d_bounds(const uint32_t* cells, size_t ncell, size_t n, uint32_t nbricks, uint32_t* bstart,
-                      uint32_t* unsorted, hipStream_t st)
+                      uint32_t* unsorted, uint32_t epoch, hipStream_t st)
 {
   if (ncell == 0) return 0;
   uint32_t grid = cdiv(ncell, 256);
   if (grid > 4096) grid = 4096;
-  k_x1d_bounds<<<grid, 256, 0, st>>>(cells, ncell, n, nbricks, bstart, unsorted);
+  k_x1d_bounds<<<grid, 256, 0, st>>>(cells, ncell, n, nbricks, bstart, unsorted, epoch);
   return (int)hipGetLastError();
 }
 
@@ -643,7 +645,7 @@ template int launch_lorenzo_x<float>(const uint16_t*, float*, size_t, size_t, si
                                      const LorenzoGeom&, hipStream_t, const X1dOutliers*);
 template int launch_lorenzo_x<double>(const uint16_t*, double*, size_t, size_t, size_t, double, int, bool,
                                       const LorenzoGeom&, hipStream_t, const X1dOutliers*);
-template int launch_scatter<float>(const uint32_t*, size_t, float*, size_t, hipStream_t, const uint32_t*);
-template int launch_scatter<double>(const uint32_t*, size_t, double*, size_t, hipStream_t, const uint32_t*);
+template int launch_scatter<float>(const uint32_t*, size_t, float*, size_t, hipStream_t, const uint32_t*, uint32_t);
+template int launch_scatter<double>(const uint32_t*, size_t, double*, size_t, hipStream_t, const uint32_t*, uint32_t);
 
 }  // namespace cusz_amd

@@ -92,6 +92,8 @@ struct Pipeline {
   uint32_t* d_spl_sps = nullptr;  // per-tile spill range starts
   uint32_t* d_spl_x = nullptr;    // decompression buckets
   uint32_t* d_x1d = nullptr;      // 1-D decompression: per-brick first outlier cell + unsorted flag
+  uint32_t cell_epoch = 0;        // tags the unsorted flag of the current decompress (never 0)
+  uint32_t next_cell_epoch() { return cell_epoch = cell_epoch + 1 ? cell_epoch + 1 : 1; }
   size_t spl_x_words = 0;
   int sublen = 256, pardeg = 1;
   int user_sublen = 0;
@@ -195,7 +197,10 @@ struct Pipeline {
     CUSZ_AMD_HIP_CHECK(hipGetDevice(&device));
     tune_chunking(n, device, &sublen, &pardeg);
     geom = lorenzo_geom(ndim, l.x, l.y, l.z, elem_bytes);
-    if (ndim == 1) CUSZ_AMD_HIP_CHECK(hipMalloc(&d_x1d, ((size_t)geom.nbricks + 2) * 4));
+    if (ndim == 1) {
+      CUSZ_AMD_HIP_CHECK(hipMalloc(&d_x1d, ((size_t)geom.nbricks + 2) * 4));
+      CUSZ_AMD_HIP_CHECK(hipMemset(d_x1d, 0, ((size_t)geom.nbricks + 2) * 4));  // unsorted word: no epoch yet
+    }
     sgeom = spline_geom(l.x, l.y, l.z);
     spl_cap = (uint32_t)(std::min<size_t>(l.x, 32) * std::min<size_t>(l.y, 8) * std::min<size_t>(l.z, 8) / 10 + 16);
     // outlier capacity: 10 % of the input like the reference (buf_comp.hh:55), as per-brick
@@ -215,7 +220,10 @@ struct Pipeline {
       CUSZ_AMD_HIP_CHECK(hipMalloc(&d_bbase, ((size_t)bl.g.nbricks + 1) * 4));
       CUSZ_AMD_HIP_CHECK(hipMalloc(&d_plan, 2 * ((size_t)brick_plan_blocks(bl.g.nbricks) + 1) * 4));
       // fused decompression: per-brick first outlier cell + unsorted flag (d_x1d's role in 1-D)
-      if (!d_x1d) CUSZ_AMD_HIP_CHECK(hipMalloc(&d_x1d, ((size_t)bl.g.nbricks + 2) * 4));
+      if (!d_x1d) {
+        CUSZ_AMD_HIP_CHECK(hipMalloc(&d_x1d, ((size_t)bl.g.nbricks + 2) * 4));
+        CUSZ_AMD_HIP_CHECK(hipMemset(d_x1d, 0, ((size_t)bl.g.nbricks + 2) * 4));
+      }
       CUSZ_AMD_HIP_CHECK(hipMalloc(&d_codes8, (size_t)bl.g.nbricks * bl.g.brick_elems + 64));  // + 8-B load slack
       CUSZ_AMD_HIP_CHECK(hipMalloc(&d_rowmask, (size_t)bl.g.nbricks * 8));
     }
@@ -646,22 +654,23 @@ struct Pipeline {
     X1dOutliers ox;  // 1-D: the reconstruction reads sorted cells directly (no scatter pass)
     if (geom.ndim == 1 && d_x1d && !zz && !brickdec && h->splen) {
       const uint32_t nb = geom.nbricks;
-      CUSZ_AMD_HIP_CHECK(hipMemsetAsync(d_x1d, 0, ((size_t)nb + 2) * 4, stream));
-      CUSZ_AMD_HIP_CHECK((hipError_t)launch_x1d_bounds(cells, h->splen, n, nb, d_x1d, d_x1d + nb + 1, stream));
-      ox = X1dOutliers{cells, (size_t)h->splen, d_x1d, d_x1d + nb + 1};
+      CUSZ_AMD_HIP_CHECK((hipError_t)launch_x1d_bounds(cells, h->splen, n, nb, d_x1d, d_x1d + nb + 1,
+                                                       next_cell_epoch(), stream));
+      ox = X1dOutliers{cells, (size_t)h->splen, d_x1d, d_x1d + nb + 1, cell_epoch};
     }
     // fused brick path: the decoder ranks each row's zero codes against the brick's cells when
     // they are grouped and sorted; only otherwise does the scatter below run (only_if = unsorted)
     BrickOutliers bo;
     if (brickdec && !zz && h->splen) {
       const uint32_t nb = bl.g.nbricks;
-      CUSZ_AMD_HIP_CHECK(hipMemsetAsync(d_x1d, 0, ((size_t)nb + 2) * 4, stream));
-      CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_cell_bounds(bl, cells, h->splen, d_x1d, d_x1d + nb + 1, stream));
-      bo = BrickOutliers{cells, (size_t)h->splen, d_x1d, d_x1d + nb + 1};
+      CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_cell_bounds(bl, cells, h->splen, d_x1d, d_x1d + nb + 1,
+                                                              next_cell_epoch(), stream));
+      bo = BrickOutliers{cells, (size_t)h->splen, d_x1d, d_x1d + nb + 1, cell_epoch};
       ox.unsorted = bo.unsorted;
+      ox.epoch = cell_epoch;
     }
     if (zz) CUSZ_AMD_HIP_CHECK(hipMemsetAsync(out, 0, n * sizeof(T), stream));
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_scatter<T>(cells, h->splen, out, n, stream, ox.unsorted));
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_scatter<T>(cells, h->splen, out, n, stream, ox.unsorted, ox.epoch));
     mark(7);
     if (brickdec) return decompress_brick<T>(h, in, out, zz, bo);
     int s = decode_codes(h, in);
