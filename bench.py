@@ -323,12 +323,14 @@ def bench_field(args, world, rank, dist, dev):
         # fused brick path (brick.hip): pass 1 reads the field once and writes brick-ordered codes,
         # the per-brick u16 histograms and the outlier cells; pass 2 (+ the plan kernel) reads the
         # codes and writes the archive; decompress is one kernel (decode + reconstruct)
-        nbricks = n // (256 * 64)
+        nbricks = -(-n // (256 * 64))
         kernels = {
-            "brick_scan": (st[cz.T_PREDICT], esz * n + 2 * n + 2 * 1024 * nbricks + 8 * splen, ["k_brick3_scan"]),
+            "brick_scan": (st[cz.T_PREDICT], esz * n + 2 * n + 2 * 1024 * nbricks + 8 * splen,
+                           ["k_brick3_scan", "k_brick1_scan"]),
             "brick_plan+pack": (st[cz.T_ENCODE], 2 * 1024 * nbricks + 2 * n + arch_bytes,
                                 ["k_brick_plan", "k_brick3_pack"]),
-            "brick_decode": (st[cz.T_DECODE] + st[cz.T_RECON], arch_bytes + esz * n, ["k_brick3_decode"]),
+            "brick_decode": (st[cz.T_DECODE] + st[cz.T_RECON], arch_bytes + esz * n,
+                             ["k_brick3_decode", "k_brick1_decode"]),
         }
     else:
         kernels = {

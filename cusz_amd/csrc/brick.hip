@@ -41,6 +41,7 @@ using namespace lrzd;
 namespace {
 
 constexpr int kBrickWaves = 4;  // waves per workgroup in the encode passes
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 // A unit = kUnitBricks consecutive bricks, processed by one wave in both encode passes: one
 // histogram record (u16 counts: a unit has at most 32768 elements), one outlier slot and one
 // reserved bitstream region per unit.
@@ -175,6 +176,57 @@ __device__ __forceinline__ void store_codes_row(uint16_t* p, const uint16_t (&q)
   *reinterpret_cast<uint2*>(p) = w;
 }
 
+// One brick row of codes between the encode passes: bytes (code - c0) when every code of the
+// row fits [c0, c0 + 254], else u16 with the row's bit set in the brick's row mask (BrickCodes).
+template <int V>
+__device__ __forceinline__ void store_brick_row(const BrickCodes& bcs, uint16_t* cbrick, uint8_t* cbrick8, int row,
+                                                const uint16_t (&qc)[V], uint64_t& rowmask)
+{
+  static_assert(V == 4, "one 4-B byte-code store per lane and row");
+  bool wide = false;
+#pragma unroll
+  for (int k = 0; k < V; k++) wide |= (uint32_t)qc[k] - bcs.c0 > 254u;
+  if (__builtin_amdgcn_ballot_w64(wide)) {
+    store_codes_row<V>(cbrick + (size_t)row * (64 * V), qc);
+    rowmask |= 1ull << row;
+  }
+  else {
+    uint32_t w = 0;
+#pragma unroll
+    for (int k = 0; k < V; k++) w |= ((uint32_t)qc[k] - bcs.c0) << (8 * k);
+    *reinterpret_cast<uint32_t*>(cbrick8 + (size_t)row * (64 * V)) = w;
+  }
+}
+
+// End of a pass-1 unit: outlier count, row mask, the unit's histogram as a u16 record (16-B
+// stores, 8 bins per lane; the wave's LDS copy is cleared) and into the workgroup histogram.
+__device__ __forceinline__ void finish_unit(const OutlierSink& ol, const BrickCodes& bcs, uint32_t u, uint32_t cnt,
+                                            uint64_t rowmask, uint32_t* s_hist, uint32_t* s_wg, uint16_t* bhist,
+                                            int hs, int lane)
+{
+  if (lane == 0) ol.brick_cnt[u] = cnt;
+  if (lane == 0) bcs.rowmask[u] = rowmask;  // kUnitBricks == 1: unit = brick
+  hfd::wave_sync();
+  uint16_t* bh = bhist + (size_t)u * hs;
+  for (int i0 = lane * 8; i0 < hs; i0 += 512) {
+    uint32_t c[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      c[k] = 0;
+#pragma unroll
+      for (int j = 0; j < kHistCopies; j++) c[k] += s_hist[(i0 + k) * kHistCopies + j];
+    }
+#pragma unroll
+    for (int k = 0; k < 8 * kHistCopies; k++) s_hist[i0 * kHistCopies + k] = 0;
+    *reinterpret_cast<uint4*>(bh + i0) =
+        make_uint4(c[0] | c[1] << 16, c[2] | c[3] << 16, c[4] | c[5] << 16, c[6] | c[7] << 16);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      if (c[k]) atomicAdd(&s_wg[i0 + k], c[k]);
+  }
+  hfd::wave_sync();
+}
+
 // =========================================================================================
 // pass 1: predict -> histograms + outliers
 // =========================================================================================
@@ -270,22 +322,7 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
 #endif
           }
 #ifndef CUSZ_AMD_SCAN_NOCODES  // (timing experiment switch: no code stores)
-          {
-            static_assert(V == 4, "one 4-B byte-code store per lane and row");
-            bool wide = false;
-#pragma unroll
-            for (int k = 0; k < V; k++) wide |= (uint32_t)qc[k] - bcs.c0 > 254u;
-            if (__builtin_amdgcn_ballot_w64(wide)) {
-              store_codes_row<V>(cbrick + (size_t)row * (64 * V), qc);
-              rowmask |= 1ull << row;
-            }
-            else {
-              uint32_t w = 0;
-#pragma unroll
-              for (int k = 0; k < V; k++) w |= ((uint32_t)qc[k] - bcs.c0) << (8 * k);
-              *reinterpret_cast<uint32_t*>(cbrick8 + (size_t)row * (64 * V)) = w;
-            }
-          }
+          store_brick_row<V>(bcs, cbrick, cbrick8, row, qc, rowmask);
 #endif
           if (anyol) {
             uint32_t mask = 0;
@@ -300,28 +337,104 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
           }
         }
     }
-    if (lane == 0) ol.brick_cnt[u] = cnt;
-    if (lane == 0) bcs.rowmask[u] = rowmask;  // kUnitBricks == 1: unit = brick
-    hfd::wave_sync();
-    // unit histogram -> u16 record (16-B stores, 8 bins per lane) and the workgroup histogram
-    uint16_t* bh = bhist + (size_t)u * hs;
-    for (int i0 = lane * 8; i0 < hs; i0 += 512) {
-      uint32_t c[8];
+    finish_unit(ol, bcs, u, cnt, rowmask, s_hist, s_wg, bhist, hs, lane);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < bklen; i += blockDim.x) {
+    const uint32_t c = s_wg[i];
+    if (c) atomicAdd(&g_hist[i], c);
+  }
+}
+
+// 1-D pass 1 (lrz_c.cuhip.inl:23-109): a brick is 64 consecutive chunks of W = 256 (16 tiles
+// of 1024), brick row r = chunk 64 b + r, so brick order is index order.  Lane l holds x in
+// [4 l, 4 l + 4) of each row; the prequant of the element before the row's first comes from lane
+// 63 of the previous row, 0 at a tile start.  Rows are loaded kScanAhead ahead (register queue,
+// raw buffer loads from the brick's origin, past the field's end they read 0); codes, histograms,
+// outlier slots and row masks as in the 3-D pass.
+template <typename T, int V, bool ZZ>
+__global__ void __launch_bounds__(64 * kBrickWaves)
+k_brick1_scan(const T* __restrict__ in, size_t n, T ebx2_r, T r, OutlierSink ol, uint32_t* __restrict__ g_hist,
+              uint16_t* __restrict__ bhist, BrickCodes bcs, int bklen, uint32_t nbricks)
+{
+  static_assert(V == 4, "W = 256");
+  extern __shared__ uint32_t smem[];
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t* s_wg = smem;
+  uint32_t* s_hist = smem + (1 + wid * kHistCopies) * kMaxBklen;
+  for (int i = threadIdx.x; i < bklen; i += blockDim.x) s_wg[i] = 0;
+  for (int i = lane; i < bhist_stride(bklen) * kHistCopies; i += 64) s_hist[i] = 0;
+  const uint32_t hc = (uint32_t)lane & (kHistCopies - 1);
+  __syncthreads();
+  const uint32_t nw = gridDim.x * kBrickWaves;
+  const int hs = bhist_stride(bklen);
+  constexpr int D = kScanAhead<T>;
+  constexpr uint32_t kBE = 64 * 64 * V;  // elements per brick
+  const uint32_t x0 = (uint32_t)lane * V;
+  auto issue_row = [&](uint32_t b, int row, T (&dst)[V]) {
+    if (b >= nbricks) return;
+    const size_t o = (size_t)b * kBE;
+    const uint32_t span = (uint32_t)(min((size_t)kBE, n - o) * sizeof(T));
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(in + o), 0, (int)span, 0x00020000);
+    const uint32_t off = ((uint32_t)row * (64 * V) + x0) * (uint32_t)sizeof(T);
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-        c[k] = 0;
-#pragma unroll
-        for (int j = 0; j < kHistCopies; j++) c[k] += s_hist[(i0 + k) * kHistCopies + j];
-      }
-#pragma unroll
-      for (int k = 0; k < 8 * kHistCopies; k++) s_hist[i0 * kHistCopies + k] = 0;
-      *reinterpret_cast<uint4*>(bh + i0) =
-          make_uint4(c[0] | c[1] << 16, c[2] | c[3] << 16, c[4] | c[5] << 16, c[6] | c[7] << 16);
-#pragma unroll
-      for (int k = 0; k < 8; k++)
-        if (c[k]) atomicAdd(&s_wg[i0 + k], c[k]);
+    for (int h = 0; h < (int)(V * sizeof(T) / 16); h++) {
+      const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + 16 * h), 0, 0);
+      __builtin_memcpy(reinterpret_cast<char*>(&dst[0]) + 16 * h, &v, 16);
     }
-    hfd::wave_sync();
+  };
+  uint32_t u = blockIdx.x * kBrickWaves + wid;
+  T q[D][V];
+#pragma unroll
+  for (int j = 0; j < D; j++) issue_row(u, j, q[j]);
+  for (; u < nbricks; u += nw) {
+    uint32_t cnt = 0;
+    uint64_t rowmask = 0;
+    const size_t bbase = (size_t)u * kBE;
+    const bool full = n - bbase >= kBE;  // no element past the field's end (uniform)
+    uint16_t* cbrick = bcs.c16 + bbase + x0;
+    uint8_t* cbrick8 = bcs.c8 + bbase + x0;
+    T carry = 0;  // prequant of the previous row's last element
+#pragma unroll 1
+    for (int r0 = 0; r0 < 64; r0 += D)
+#pragma unroll
+      for (int j = 0; j < D; j++) {
+        const int row = r0 + j;
+        T p[V];
+#pragma unroll
+        for (int k = 0; k < V; k++) p[k] = dround(q[j][k] * ebx2_r);
+        if (row + D < 64) issue_row(u, row + D, q[j]);
+        else issue_row(u + nw, row + D - 64, q[j]);
+        const size_t base = bbase + (size_t)row * (64 * V);
+        T west = __shfl_up(p[V - 1], 1);
+        const T last = __shfl(p[V - 1], 63);
+        if (lane == 0) west = (row & 3) ? carry : T(0);
+        carry = last;
+        if (!full && base >= n) continue;  // past the field's end (uniform)
+        T d[V];
+#pragma unroll
+        for (int k = V - 1; k > 0; k--) d[k] = p[k] - p[k - 1];
+        d[0] = p[0] - west;
+        float olv[V];
+        uint16_t qc[V];
+        uint32_t mask = 0;
+#pragma unroll
+        for (int k = 0; k < V; k++) {
+          bool is_ol;
+          qc[k] = quantize<T, ZZ>(d[k], r, is_ol, olv[k]);
+          const bool inr = full || base + x0 + k < n;
+          if (inr) atomicAdd(&s_hist[qc[k] * kHistCopies + hc], 1u);
+          mask |= (uint32_t)(inr && is_ol) << k;
+        }
+        store_brick_row<V>(bcs, cbrick, cbrick8, row, qc, rowmask);
+        if (__builtin_amdgcn_ballot_w64(mask != 0)) {
+          size_t idx[V];
+#pragma unroll
+          for (int k = 0; k < V; k++) idx[k] = base + x0 + k;
+          emit_outliers<V>(ol, u, cnt, mask, olv, idx);
+        }
+      }
+    finish_unit(ol, bcs, u, cnt, rowmask, s_hist, s_wg, bhist, hs, lane);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < bklen; i += blockDim.x) {
@@ -383,7 +496,7 @@ __global__ void __launch_bounds__(kPlanThreads) k_brick_plan(BrickPlanArgs a, He
       wbits += bits;
       uint32_t rows = 0;  // chunks of the unit: each may end with a partial cell
       for (uint32_t b = brick * kUnitBricks; b < min((brick + 1) * kUnitBricks, a.nbricks); b++)
-        rows += brick_rows3(b, a.nbx, a.nby, a.ly, a.lz);
+        rows += a.nd == 1 ? min(64u, a.nchunks - 64u * b) : brick_rows3(b, a.nbx, a.nby, a.ly, a.lz);
       ub = (bits + 31u * rows) >> 5;
       oc = min(a.brick_cnt[brick], a.cap_per_brick);
     }
@@ -455,7 +568,7 @@ constexpr int pack_cells_words()
 // (b * 64 + r) * W): per row, codewords -> wave scan of their lengths -> MSB-first packing into
 // LDS cells (each row starts a new cell, hf_kernels.cuhip.inl:97-157) -> one coalesced copy.
 // The codes of the next y-step are loaded while the current one is packed.
-template <int V>
+template <int V, int ND>
 __global__ void __launch_bounds__(64 * kBrickWaves)
 k_brick3_pack(BrickCodes bcs, uint32_t ly, uint32_t lz, const uint32_t* __restrict__ book,
               int bklen, BrickPlanArgs pl, uint32_t* __restrict__ par_nbit, uint32_t* __restrict__ par_entry,
@@ -501,7 +614,10 @@ k_brick3_pack(BrickCodes bcs, uint32_t ly, uint32_t lz, const uint32_t* __restri
     for (uint32_t brick = unit * kUnitBricks; brick < bend; brick++) {
       const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
       const uint32_t y0 = by * 8, z0 = bz * 8;
-      const uint32_t nyv = min(8u, ly - y0), nzv = min(8u, lz - z0);
+      // 1-D: rows [0, nrow) of the brick are chunks 64 brick + row (row = 8 y + z)
+      const uint32_t nrow = ND == 1 ? min(64u, pl.nchunks - 64u * brick) : 64u;
+      const uint32_t nyv = ND == 1 ? (nrow + 7u) / 8u : min(8u, ly - y0), nzv = ND == 1 ? 8u : min(8u, lz - z0);
+      auto row_ok = [&](uint32_t y, uint32_t z) { return ND == 1 ? y * 8u + z < nrow : z < nzv; };
       const uint8_t* src16 = reinterpret_cast<const uint8_t*>(bcs.c16 + (size_t)brick * 64 * (64 * V)) + lane * 8;
       const uint8_t* src8 = bcs.c8 + (size_t)brick * 64 * (64 * V) + lane * 4;
       const uint64_t rm = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bcs.rowmask[brick]) & 0xFFFFFFFFull) |
@@ -517,16 +633,16 @@ k_brick3_pack(BrickCodes bcs, uint32_t ly, uint32_t lz, const uint32_t* __restri
       uint32_t my_nbit = 0, my_entry = 0;
       uint2 cur[8], nxt[8];
 #pragma unroll
-      for (int z = 0; z < 8; z++) nxt[z] = (uint32_t)z < nzv ? load_row(z) : make_uint2(0, 0);
+      for (int z = 0; z < 8; z++) nxt[z] = row_ok(0, z) ? load_row(z) : make_uint2(0, 0);
       for (uint32_t y = 0; y < nyv; y++) {
 #pragma unroll
         for (int z = 0; z < 8; z++) cur[z] = nxt[z];
         if (y + 1 < nyv)
 #pragma unroll
-          for (int z = 0; z < 8; z++) nxt[z] = (uint32_t)z < nzv ? load_row((y + 1) * 8 + z) : make_uint2(0, 0);
+          for (int z = 0; z < 8; z++) nxt[z] = row_ok(y + 1, z) ? load_row((y + 1) * 8 + z) : make_uint2(0, 0);
 #pragma unroll
         for (int z = 0; z < 8; z++) {
-          if ((uint32_t)z >= nzv) break;
+          if (!row_ok(y, z)) break;
           uint32_t qs[4];
           if ((rm >> (y * 8 + z)) & 1ull) {
             qs[0] = cur[z].x & 0xFFFFu, qs[1] = cur[z].x >> 16, qs[2] = cur[z].y & 0xFFFFu, qs[3] = cur[z].y >> 16;
@@ -536,9 +652,13 @@ k_brick3_pack(BrickCodes bcs, uint32_t ly, uint32_t lz, const uint32_t* __restri
             for (int k = 0; k < 4; k++) qs[k] = ((cur[z].x >> (8 * k)) & 255u) + bcs.c0;
           }
           uint32_t w[V], bits = 0;
+          // 1-D: the field's last chunk may be short; codes past its end get no codeword
+          const size_t cfirst = ((size_t)brick * 64u + y * 8u + (uint32_t)z) * (64u * V);
+          const bool short_row = ND == 1 && pl.n - cfirst < 64u * V;
 #pragma unroll
           for (int k = 0; k < V; k++) {
             w[k] = s_book[qs[k]];
+            if (short_row && cfirst + (uint32_t)lane * V + k >= pl.n) w[k] = 0;
             bits += w[k] >> 27;
           }
           const uint32_t inc = hfd::wave_incl_scan(bits);
@@ -559,8 +679,8 @@ k_brick3_pack(BrickCodes bcs, uint32_t ly, uint32_t lz, const uint32_t* __restri
         }
       }
       const uint32_t ry = lane >> 3, rz = lane & 7;
-      if (ry < nyv && rz < nzv) {
-        const size_t c = ((size_t)(z0 + rz) * ly + (y0 + ry)) * nbx + bx;
+      if (row_ok(ry, rz) && ry < nyv) {
+        const size_t c = ND == 1 ? (size_t)brick * 64u + (uint32_t)lane : ((size_t)(z0 + rz) * ly + (y0 + ry)) * nbx + bx;
         par_nbit[c] = my_nbit;
         par_entry[c] = my_entry;
       }
@@ -856,6 +976,145 @@ __global__ void __launch_bounds__(256) k_brick_cell_bounds(const uint32_t* __res
   }
 }
 
+#ifdef CUSZ_AMD_DEC_PROFILE
+#define BPROF_P , unsigned long long(&pc)[8], unsigned long long &tk, unsigned long long &tp
+#define BPROF_A , pc, tk, tp
+#else
+#define BPROF_P
+#define BPROF_A
+#endif
+
+// One wave's decoder state that outlives a chunk: bitstream resource, the lane's ring column, the
+// code tile.
+struct DecWave {
+  __amdgpu_buffer_rsrc_t rbits;
+  uint32_t* ring_lane;
+  uint16_t* tile;
+  uint32_t ubk;
+  int lane;
+};
+
+// Decode one chunk per lane (chunk bits at word vbase / 4, nbit bits, vlen <= 256 symbols; a dead
+// lane decodes nothing) in W / kBlk blocks of kBlk columns into the tile; after each block the
+// wave calls recon(blk).  pro() runs while the first words are in flight; blk_start(blk) before
+// each block's decode.
+template <class Pro, class BlkStart, class Recon>
+__device__ __forceinline__ void decode_chunks(const hfd::LdsTables<kDecB>& tb, const hfd::DecRegs& rg,
+                                              const DecWave& dw, bool live, uint32_t vbase, uint32_t nbit,
+                                              uint32_t vlen, Pro&& pro, BlkStart&& blk_start,
+                                              Recon&& recon BPROF_P)
+{
+  constexpr uint32_t W = 256;
+  const int lane = dw.lane;
+  uint32_t* ring_lane = dw.ring_lane;
+  const uint32_t nwords = (nbit + 31u) >> 5;
+  // words 0..7 (0..2 into registers, 2..7 into the ring), issued before pro()
+  const u32x4 a0 = __builtin_amdgcn_raw_buffer_load_b128(dw.rbits, (int)(live ? vbase : kOOB), 0, 0);
+  const u32x4 a1 = __builtin_amdgcn_raw_buffer_load_b128(dw.rbits, (int)(live ? vbase + 16u : kOOB), 0, 0);
+  pro();
+  uint32_t w0 = 0, w1 = a0.x, w2 = a0.y, nx = a0.z;
+  ring_lane[2 * 64] = a0.z;  // nx is re-read every step, also by a first step that does not move
+  ring_lane[3 * 64] = a0.w;
+  ring_lane[4 * 64] = a1.x, ring_lane[5 * 64] = a1.y, ring_lane[6 * 64] = a1.z, ring_lane[7 * 64] = a1.w;
+  uint32_t kk = 2;    // word index held by nx
+  uint32_t ctop = 8;  // words [0, ctop) have been written (ring or registers)
+  uint32_t ltop = 8;  // words [0, ltop) have been requested
+  uint32_t sh = 0;    // 32 - bits of w0 consumed
+  uint32_t cnt = live ? 0u : 0x40000000u;  // symbols decoded; a dead lane never steps
+  uint32_t keep = 0;  // symbol at the even column before an odd cnt (see the tile stores)
+  uint32_t rdy = ctop >= nwords ? 0xFFFFFFFFu : ctop;  // words [0, rdy) are readable
+  u32x4 pa, pb;       // groups in flight
+  bool fa = false, fb = false;
+  BPROF(hfd::wave_sync(); tk = __builtin_readcyclecounter(); pc[1] += tk - tp; tp = tk;)
+
+  auto issue = [&](u32x4& p, bool& f) {
+    const bool ok = ltop < nwords && ltop + 4u <= kk + kRing;  // never over a word still needed
+    p = __builtin_amdgcn_raw_buffer_load_b128(dw.rbits, (int)(ok ? vbase + ltop * 4u : kOOB), 0, 0);
+    f = ok;
+    ltop += ok ? 4u : 0u;
+  };
+  // Write a landed group into the ring.  The stores are unconditional (a lane without a group
+  // writes the junk slot kRing), so the compiler's wait for the load sits here on every path and
+  // no load is left pending past the block's end.
+  auto consume = [&](const u32x4& p, bool& f) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) ring_lane[(f ? ((ctop + (uint32_t)i) & (kRing - 1u)) : kRing) * 64] = p[i];
+    ctop += f ? 4u : 0u;
+    f = false;
+    rdy = ctop >= nwords ? 0xFFFFFFFFu : ctop;
+  };
+
+  for (int blk = 0; blk < (int)(W / kBlk); blk++) {
+    blk_start(blk);
+    uint16_t* rowp = dw.tile + lane * kTP - blk * kBlk;  // rowp[cnt] = tile column cnt - 64 blk
+    const uint32_t target = min((uint32_t)(blk + 1) * kBlk, vlen);
+    auto quarter = [&]() {
+      BPROF(pc[6] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(cnt < target && !(kk + (uint32_t)kF + 1u < rdy)));
+            pc[7] += kF * __builtin_popcountll(__builtin_amdgcn_ballot_w64(cnt < target && kk + (uint32_t)kF + 1u < rdy));)
+      if (cnt < target && kk + (uint32_t)kF + 1u < rdy) {  // at most one word crossed per step
+        uint32_t e = 0;
+        auto step = [&](bool lng) {
+          const uint32_t win = __builtin_amdgcn_alignbit(w0, w1, sh);  // chunk bits [pos, pos + 32)
+          // a code longer than 16 bits has no table entry: e = 0 consumes nothing, and the lane
+          // decodes it after the quarter (rare: no branch in the steps)
+          e = lng ? hfd::lookup_long<kDecB>(tb, rg, win, dw.ubk) : hfd::lookup_short<kDecB>(tb, rg, win);
+          const uint32_t sy = e & hfd::kEntSymMask;
+          const bool odd = cnt & 1u;
+          *reinterpret_cast<uint32_t*>(rowp + (cnt & ~1u)) = odd ? (keep | (sy << 16)) : sy;
+          keep = e == 0 ? keep : (odd ? (sy >> 16) : (sy & 0xFFFFu));
+          cnt += hfd::ent_nsym(e);
+          const int32_t s2 = (int32_t)sh - (int32_t)hfd::ent_bits(e);
+          const bool shf = s2 < 0;  // crossed into the next word
+          sh = (uint32_t)s2 & 31u;
+          w0 = shf ? w1 : w0;
+          w1 = shf ? w2 : w1;
+          w2 = shf ? nx : w2;
+          kk += shf ? 1u : 0u;
+          nx = ring_lane[(kk & (kRing - 1u)) * 64];
+        };
+#pragma unroll
+        for (int st = 0; st < kF; st++) step(false);
+        if (__builtin_amdgcn_ballot_w64(e == 0)) {  // a lane met a long code: one slow step
+          if (e == 0) step(true);
+        }
+      }
+    };
+    // a group is written into the ring two refills after its load; the first wait of a block
+    // comes 2 kF steps after the previous block's stores
+    issue(pa, fa);
+    quarter();
+    issue(pb, fb);
+    quarter();
+    do {
+      consume(pa, fa);
+      issue(pa, fa);
+      quarter();
+      consume(pb, fb);
+      issue(pb, fb);
+      quarter();
+      BPROF(pc[5]++;)
+    } while (__builtin_amdgcn_ballot_w64(cnt < target));
+    BPROF(hfd::wave_sync(); tk = __builtin_readcyclecounter(); pc[2] += tk - tp; tp = tk;)
+    consume(pa, fa);  // drain: nothing stays in flight across the stores below
+    consume(pb, fb);
+    hfd::wave_sync();
+    BPROF(tk = __builtin_readcyclecounter(); pc[3] += tk - tp; tp = tk;)
+    recon(blk);
+    hfd::wave_sync();
+    // symbols decoded past the block end move to its front (`keep` carries a pending one)
+    {
+      uint32_t* rw = reinterpret_cast<uint32_t*>(dw.tile + lane * kTP);
+      uint32_t v[kF + 1];
+#pragma unroll
+      for (int i = 0; i <= kF; i++) v[i] = rw[kBlk / 2 + i];
+#pragma unroll
+      for (int i = 0; i <= kF; i++) rw[i] = v[i];
+    }
+    hfd::wave_sync();
+    BPROF(tk = __builtin_readcyclecounter(); pc[4] += tk - tp; tp = tk;)
+  }
+}
+
 template <typename T, bool ZZ, bool BUF>
 __global__ void __launch_bounds__(64 * kDecWaves)
 k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const uint8_t* __restrict__ revbook,
@@ -869,15 +1128,13 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
   const hfd::DecRegs rg = hfd::load_dec_regs(tb);
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* wbase = dsm + (size_t)wid * kDecWaveBytes;
-  uint32_t* ring_lane = reinterpret_cast<uint32_t*>(wbase) + lane;
   uint16_t* tile = reinterpret_cast<uint16_t*>(wbase + kDecTile);
   uint32_t* cval = reinterpret_cast<uint32_t*>(wbase + kDecCells);
   BrickCells bc{cval, 1, reinterpret_cast<uint32_t*>(wbase + kDecRows), reinterpret_cast<uint32_t*>(wbase + kDecRows) + 65};
   const bool ranked = !ZZ && (ol.ncell == 0 || *ol.unsorted != ol.epoch);
-  const __amdgpu_buffer_rsrc_t rbits =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(bitstream), 0, (int)(bs_words * 4u), (int)kBufRsrcW3);
+  const DecWave dw{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(bitstream), 0, (int)(bs_words * 4u), (int)kBufRsrcW3),
+                   reinterpret_cast<uint32_t*>(wbase) + lane, tile, (uint32_t)bklen, lane};
   const size_t plane = (size_t)lx * ly;
-  const uint32_t ubk = (uint32_t)bklen;
   constexpr uint32_t W = 256;
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
   const uint32_t ry = (uint32_t)lane >> 3, rz = (uint32_t)lane & 7u;
@@ -891,12 +1148,9 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
     const size_t c = ((size_t)(z0 + rz) * ly + (y0 + ry)) * nbx + bx;
     const uint32_t nbit = live ? par_nbit[c] : 0u;
     const uint32_t vbase = (live ? par_entry[c] : 0u) * 4u;
-    const uint32_t nwords = (nbit + 31u) >> 5;
-    // words 0..7 (0..2 into registers, 2..7 into the ring), issued before the cells are read
-    const u32x4 a0 = __builtin_amdgcn_raw_buffer_load_b128(rbits, (int)(live ? vbase : kOOB), 0, 0);
-    const u32x4 a1 = __builtin_amdgcn_raw_buffer_load_b128(rbits, (int)(live ? vbase + 16u : kOOB), 0, 0);
     // the brick's outlier cells [cb, ce): per-row counts -> row starts; values into LDS
-    if (ranked) {
+    auto pro = [&]() {
+      if (!ranked) return;
       uint32_t cb = 0, ce = 0;
       if (ol.ncell) cb = ol.bstart[brick], ce = ol.bstart[brick + 1];
       const uint32_t nc = ce - cb;
@@ -916,117 +1170,205 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
       bc.carry[lane] = 0;
       bc.val = nc <= kCellCap ? cval : ol.cells + 2 * (size_t)cb;
       bc.vstride = nc <= kCellCap ? 1u : 2u;
-    }
-    uint32_t w0 = 0, w1 = a0.x, w2 = a0.y, nx = a0.z;
-    ring_lane[2 * 64] = a0.z;  // nx is re-read every step, also by a first step that does not move
-    ring_lane[3 * 64] = a0.w;
-    ring_lane[4 * 64] = a1.x, ring_lane[5 * 64] = a1.y, ring_lane[6 * 64] = a1.z, ring_lane[7 * 64] = a1.w;
-    uint32_t kk = 2;    // word index held by nx
-    uint32_t ctop = 8;  // words [0, ctop) have been written (ring or registers)
-    uint32_t ltop = 8;  // words [0, ltop) have been requested
-    uint32_t sh = 0;    // 32 - bits of w0 consumed
-    uint32_t cnt = live ? 0u : 0x40000000u;  // symbols decoded; a dead lane never steps
-    uint32_t keep = 0;  // symbol at the even column before an odd cnt (see the tile stores)
-    uint32_t rdy = ctop >= nwords ? 0xFFFFFFFFu : ctop;  // words [0, rdy) are readable
-    u32x4 pa, pb;       // groups in flight
-    bool fa = false, fb = false;
-    BPROF(hfd::wave_sync(); tk = __builtin_readcyclecounter(); pc[1] += tk - tp; tp = tk;)
-
-    auto issue = [&](u32x4& p, bool& f) {
-      const bool ok = ltop < nwords && ltop + 4u <= kk + kRing;  // never over a word still needed
-      p = __builtin_amdgcn_raw_buffer_load_b128(rbits, (int)(ok ? vbase + ltop * 4u : kOOB), 0, 0);
-      f = ok;
-      ltop += ok ? 4u : 0u;
     };
-    // Write a landed group into the ring.  The stores are unconditional (a lane without a group
-    // writes the junk slot kRing), so the compiler's wait for the load sits here on every path and
-    // no load is left pending past the block's end.
-    auto consume = [&](const u32x4& p, bool& f) {
-#pragma unroll
-      for (int i = 0; i < 4; i++) ring_lane[(f ? ((ctop + (uint32_t)i) & (kRing - 1u)) : kRing) * 64] = p[i];
-      ctop += f ? 4u : 0u;
-      f = false;
-      rdy = ctop >= nwords ? 0xFFFFFFFFu : ctop;
+    auto recon = [&](int blk) {
+      const uint32_t nyv = min(8u, ly - y0), nzv = min(8u, lz - z0);
+      const size_t base_elem = (size_t)z0 * plane + (size_t)y0 * lx + (size_t)bx * W + (size_t)blk * kBlk;
+      if (ranked)
+        recon_block<T, ZZ, BUF, kTP, true>(tile, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane, &bc);
+      else
+        recon_block<T, ZZ, BUF, kTP, false>(tile, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane);
     };
-
-    for (int blk = 0; blk < (int)(W / kBlk); blk++) {
-      uint16_t* rowp = tile + lane * kTP - blk * kBlk;  // rowp[cnt] = tile column cnt - 64 blk
-      const uint32_t target = (uint32_t)(blk + 1) * kBlk;
-      auto quarter = [&]() {
-        BPROF(pc[6] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(cnt < target && !(kk + (uint32_t)kF + 1u < rdy)));
-              pc[7] += kF * __builtin_popcountll(__builtin_amdgcn_ballot_w64(cnt < target && kk + (uint32_t)kF + 1u < rdy));)
-        if (cnt < target && kk + (uint32_t)kF + 1u < rdy) {  // at most one word crossed per step
-          uint32_t e = 0;
-          auto step = [&](bool lng) {
-            const uint32_t win = __builtin_amdgcn_alignbit(w0, w1, sh);  // chunk bits [pos, pos + 32)
-            // a code longer than 16 bits has no table entry: e = 0 consumes nothing, and the lane
-            // decodes it after the quarter (rare: no branch in the steps)
-#ifdef CUSZ_AMD_TESTA
-            e = hfd::lookup1<kDecB>(tb, rg, win, ubk);
-#else
-            e = lng ? hfd::lookup_long<kDecB>(tb, rg, win, ubk) : hfd::lookup_short<kDecB>(tb, rg, win);
+    decode_chunks(tb, rg, dw, live, vbase, nbit, W, pro, [](int) {}, recon BPROF_A);
+  }
+#ifdef CUSZ_AMD_DEC_PROFILE
+  if (lane == 0)
+    for (int i = 0; i < 8; i++) atomicAdd(&g_brick_prof[i], pc[i]);
 #endif
-            const uint32_t sy = e & hfd::kEntSymMask;
-            const bool odd = cnt & 1u;
-            *reinterpret_cast<uint32_t*>(rowp + (cnt & ~1u)) = odd ? (keep | (sy << 16)) : sy;
-            keep = e == 0 ? keep : (odd ? (sy >> 16) : (sy & 0xFFFFu));
-            cnt += hfd::ent_nsym(e);
-            const int32_t s2 = (int32_t)sh - (int32_t)hfd::ent_bits(e);
-            const bool shf = s2 < 0;  // crossed into the next word
-            sh = (uint32_t)s2 & 31u;
-            w0 = shf ? w1 : w0;
-            w1 = shf ? w2 : w1;
-            w2 = shf ? nx : w2;
-            kk += shf ? 1u : 0u;
-            nx = ring_lane[(kk & (kRing - 1u)) * 64];
-          };
+}
+// ---- 1-D: fused decode + reconstruct -------------------------------------------------------
+// A wave owns a unit of 64 tiles of 1024 (4 chunks of 256 each); lane l owns tile 64 u + l and
+// decodes its four chunks in four phases (phase p: chunk 4 t + p), so a reconstruction block
+// holds, for every tile of the unit, the same 64 columns of chunk p.  The reference's 1-D order
+// (lrz_x.cuhip.inl:11-78, wave32.cuhip.inl:7-66: per thread 4 sequential elements, Hillis-Steele
+// over the 32 thread totals of each 128-element segment, then a serial sum of the segment totals)
+// runs per block with lane = (row 4 i + l / 16, group l % 16): a block is half a segment -- the
+// first half's raw thread totals stay in registers for the second half's scan (stages d = 1..8 in
+// DPP rows of 16 lanes, the lanes below d reading the first half by row_ror), and the serial
+// segment carry of each tile stays in registers across the phases.
+//
+// Outliers (archive cells in index order, k_x1d_bounds with chunk granularity): each lane
+// prefetches the next kCellPf cell values of its chunk at a block's start (they land while the
+// block decodes) and the reconstruction ranks each row's zero codes against them; ranks past the
+// prefetch read the cell directly.
+constexpr uint32_t kCellPf = 8;
+constexpr size_t kD1Cur = kDecTile + (size_t)64 * kTP * 2;  // cursor[64] | end[64] | values[64][kCellPf]
+constexpr size_t kD1WaveBytes = kD1Cur + (size_t)(2 * 64 + 64 * kCellPf) * 4;
+constexpr int kD1MaxWaves = (int)((160 * 1024 - sizeof(hfd::LdsTables<kDecB>)) / kD1WaveBytes);
+static_assert(kD1MaxWaves >= 4, "LDS");
+
+template <int CTRL, typename T>
+__device__ __forceinline__ T dpp16(T v)  // DPP row op within 16-lane rows; lanes without a source read 0
+{
+  return dppf<CTRL, 0xf>(v);
+}
+
+template <typename T, bool ZZ>
+__global__ void __launch_bounds__(64 * kDecWaves)
+k_brick1_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const uint8_t* __restrict__ revbook,
+                int bklen, const uint32_t* __restrict__ par_nbit, const uint32_t* __restrict__ par_entry, T* out,
+                size_t n, T ebx2, T r, uint32_t nchunks, uint32_t nunits, BrickOutliers ol)
+{
+  __shared__ hfd::LdsTables<kDecB> tb;
+  extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
+  hfd::build_tables<kDecB>(tb, revbook, bklen);
+  const hfd::DecRegs rg = hfd::load_dec_regs(tb);
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* wbase = dsm + (size_t)wid * kD1WaveBytes;
+  uint16_t* tile = reinterpret_cast<uint16_t*>(wbase + kDecTile);
+  uint32_t* cur = reinterpret_cast<uint32_t*>(wbase + kD1Cur);  // next cell of each row's chunk
+  uint32_t* cend = cur + 64;
+  uint32_t* cvals = cend + 64;
+  const bool ranked = !ZZ && (ol.ncell == 0 || *ol.unsorted != ol.epoch);  // else: values in `out` (scatter)
+  const uint32_t npf = ol.ncell < (1u << 28) ? kCellPf : 0u;  // prefetched ranks (32-bit buffer offsets)
+  const DecWave dw{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(bitstream), 0, (int)(bs_words * 4u), (int)kBufRsrcW3),
+                   reinterpret_cast<uint32_t*>(wbase) + lane, tile, (uint32_t)bklen, lane};
+  const __amdgpu_buffer_rsrc_t rcells = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint32_t*>(ol.cells), 0, (int)min(ol.ncell * 8, (size_t)0x7FFFFFFF), (int)kBufRsrcW3);
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  const uint32_t g = (uint32_t)lane & 15u, rsub = (uint32_t)lane >> 4;
+  const uint64_t rowbits = 0xFFFFull << (lane & 48), lt = (1ull << lane) - 1ull;
+  BPROF(unsigned long long pc[8] = {}; unsigned long long tk = __builtin_readcyclecounter(), tp = tk;)
+  for (uint32_t u = blockIdx.x * (blockDim.x >> 6) + wid; u < nunits; u += nw) {
+    T carr[16], fh[16];  // per recon row 4 i + rsub: tile carry; first-half raw totals
 #pragma unroll
-          for (int st = 0; st < kF; st++) step(false);
-          if (__builtin_amdgcn_ballot_w64(e == 0)) {  // a lane met a long code: one slow step
-            if (e == 0) step(true);
+    for (int i = 0; i < 16; i++) carr[i] = T(0);
+    const bool full = (size_t)(u + 1) * 65536u <= n;  // every element of the unit is in the field
+    for (uint32_t p = 0; p < 4; p++) {
+      BPROF(pc[0]++; tp = __builtin_readcyclecounter();)
+      const size_t c = ((size_t)u * 64u + (uint32_t)lane) * 4u + p;
+      const bool live = c < nchunks;
+      const uint32_t nbit = live ? par_nbit[c] : 0u;
+      const uint32_t vbase = (live ? par_entry[c] : 0u) * 4u;
+      const uint32_t vlen = live ? (uint32_t)min((size_t)256, n - c * 256u) : 0u;
+      u32x4 pf[kCellPf / 2];
+      auto pro = [&]() {
+        if (!ranked) return;
+        cur[lane] = live && ol.ncell ? ol.bstart[c] : 0u;
+        cend[lane] = live && ol.ncell ? ol.bstart[c + 1] : 0u;
+      };
+      auto blk_start = [&](int) {
+        if (!ranked) return;
+        const uint32_t cb = cur[lane];
+#pragma unroll
+        for (int h = 0; h < (int)kCellPf / 2; h++)
+          pf[h] = __builtin_amdgcn_raw_buffer_load_b128(rcells, (int)(live && npf ? cb * 8u + 16u * h : kOOB), 0, 0);
+      };
+      auto recon = [&](int blk) {
+        if (ranked) {
+#pragma unroll
+          for (int h = 0; h < (int)kCellPf / 2; h++) {
+            cvals[lane * kCellPf + 2 * h] = pf[h].x;
+            cvals[lane * kCellPf + 2 * h + 1] = pf[h].z;
           }
+          hfd::wave_sync();
+        }
+        const bool odd = blk & 1;
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+          const uint32_t R = 4u * i + rsub;
+          const uint32_t* tr = reinterpret_cast<const uint32_t*>(tile + R * kTP) + 2 * g;
+          const uint32_t c01 = tr[0], c23 = tr[1];
+          const uint32_t cd[4] = {c01 & 0xFFFFu, c01 >> 16, c23 & 0xFFFFu, c23 >> 16};
+          const size_t e0 = (((size_t)u * 64u + R) * 4u + p) * 256u + (uint32_t)blk * kBlk + 4u * g;
+          T v[4];
+#pragma unroll
+          for (int k = 0; k < 4; k++) v[k] = ZZ ? (T)zz_dec((uint16_t)cd[k]) : (T)cd[k] - r;
+          if (ranked) {
+            bool z[4];
+            uint64_t m[4];
+            uint32_t below = 0, tot = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+              z[k] = cd[k] == 0u;
+              m[k] = __builtin_amdgcn_ballot_w64(z[k]);
+              below += (uint32_t)__builtin_popcountll(m[k] & rowbits & lt);
+              tot += (uint32_t)__builtin_popcountll(m[k] & rowbits);
+            }
+            if (m[0] | m[1] | m[2] | m[3]) {
+              const uint32_t cb = cur[R], ce = cend[R];
+              uint32_t rk = below;
+#pragma unroll
+              for (int k = 0; k < 4; k++) {
+                if (z[k]) {
+                  const uint32_t j = cb + rk;
+                  T o = T(0);
+                  if (j < ce) o = (T)__builtin_bit_cast(float, rk < npf ? cvals[R * kCellPf + rk] : ol.cells[2 * (size_t)j]);
+                  v[k] = o - r;  // (o + 0) - r
+                  rk++;
+                }
+              }
+              hfd::wave_sync();
+              if (g == 0) cur[R] = cb + tot;
+            }
+          }
+          else if (__builtin_amdgcn_ballot_w64(cd[0] == 0u || cd[1] == 0u || cd[2] == 0u || cd[3] == 0u)) {
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+              if (cd[k] == 0u) {
+                const T o = (full || e0 + k < n) ? out[e0 + k] : T(0);
+                v[k] = ZZ ? o + v[k] : o - r;  // plane + zz_dec(0), or (plane + 0) - r
+              }
+          }
+          // per thread: 4 sequential elements (wave32.cuhip.inl:10)
+          v[1] = v[1] + v[0];
+          v[2] = v[2] + v[1];
+          v[3] = v[3] + v[2];
+          // thread totals: Hillis-Steele over the segment's 32 (wave32.cuhip.inl:14-17)
+          T prev;
+          if (!odd) {
+            T a = v[3];
+            fh[i] = a;
+            a = a + dpp16<0x111>(a);
+            a = a + dpp16<0x112>(a);
+            a = a + dpp16<0x114>(a);
+            a = a + dpp16<0x118>(a);
+            prev = dpp16<0x111>(a);  // group 0 of the segment adds nothing
+          }
+          else {
+            // group 16 + g reads group 16 + g - d: lane g - d of b, or lane g - d + 16 of f.  The
+            // choice is made on the source side (lane s < 16 - d offers b, the others f) so the
+            // DPP rotate runs with every lane active (a select of two DPP results may be turned
+            // into a branch, and a DPP under a partial exec mask reads 0 from inactive lanes)
+            T f = fh[i], b = v[3];
+#define D1_STAGE(D)                                                                   \
+  {                                                                                   \
+    const T bs = dpp16<0x120 + (D)>(g < 16u - (D) ? b : f);                           \
+    f = f + dpp16<0x110 + (D)>(f);                                                    \
+    b = b + bs;                                                                       \
+  }
+            D1_STAGE(1) D1_STAGE(2) D1_STAGE(4) D1_STAGE(8)
+#undef D1_STAGE
+            b = b + f;  // d = 16: group 16 + g adds group g
+            prev = dpp16<0x121>(g == 15u ? f : b);  // group 15 + g: f[15] for g = 0, else b[g - 1]
+          }
+#pragma unroll
+          for (int k = 0; k < 4; k++) v[k] = v[k] + prev;
+          // serial sum of the segment totals (wave32.cuhip.inl:38-42): this segment's carry
+          const T cin = carr[i];
+          if (odd) carr[i] = cin + __shfl(v[3], (lane & 48) | 15);
+          T o[4];
+#pragma unroll
+          for (int k = 0; k < 4; k++) o[k] = (v[k] + cin) * ebx2;
+          if (full || e0 + 4 <= n)
+            store_row<T, 4>(out, e0, 0, 4, true, o);
+          else
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+              if (e0 + k < n) out[e0 + k] = o[k];
         }
       };
-      // a group is written into the ring two refills after its load; the first wait of a block
-      // comes 2 kF steps after the previous block's stores
-      issue(pa, fa);
-      quarter();
-      issue(pb, fb);
-      quarter();
-      do {
-        consume(pa, fa);
-        issue(pa, fa);
-        quarter();
-        consume(pb, fb);
-        issue(pb, fb);
-        quarter();
-        BPROF(pc[5]++;)
-      } while (__builtin_amdgcn_ballot_w64(cnt < target));
-      BPROF(hfd::wave_sync(); tk = __builtin_readcyclecounter(); pc[2] += tk - tp; tp = tk;)
-      consume(pa, fa);  // drain: nothing stays in flight across the stores below
-      consume(pb, fb);
-      hfd::wave_sync();
-      BPROF(tk = __builtin_readcyclecounter(); pc[3] += tk - tp; tp = tk;)
-      {
-        const uint32_t nyv = min(8u, ly - y0), nzv = min(8u, lz - z0);
-        const size_t base_elem = (size_t)z0 * plane + (size_t)y0 * lx + (size_t)bx * W + (size_t)blk * kBlk;
-        if (ranked)
-          recon_block<T, ZZ, BUF, kTP, true>(tile, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane, &bc);
-        else
-          recon_block<T, ZZ, BUF, kTP, false>(tile, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane);
-      }
-      hfd::wave_sync();
-      // symbols decoded past the block end move to its front (`keep` carries a pending one)
-      {
-        uint32_t* rw = reinterpret_cast<uint32_t*>(tile + lane * kTP);
-        uint32_t v[kF + 1];
-#pragma unroll
-        for (int i = 0; i <= kF; i++) v[i] = rw[kBlk / 2 + i];
-#pragma unroll
-        for (int i = 0; i <= kF; i++) rw[i] = v[i];
-      }
-      hfd::wave_sync();
-      BPROF(tk = __builtin_readcyclecounter(); pc[4] += tk - tp; tp = tk;)
+      decode_chunks(tb, rg, dw, live, vbase, nbit, vlen, pro, blk_start, recon BPROF_A);
     }
   }
 #ifdef CUSZ_AMD_DEC_PROFILE
@@ -1034,6 +1376,7 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
     for (int i = 0; i < 8; i++) atomicAdd(&g_brick_prof[i], pc[i]);
 #endif
 }
+
 }  // namespace
 
 // =========================================================================================
@@ -1045,6 +1388,17 @@ BrickGeom brick_geom(int ndim, size_t lx, size_t ly, size_t lz, int elem_bytes)
   BrickGeom g{};
   g.V = 4;  // W = 256: f32 16-B loads, f64 32-B loads per lane
   g.W = 64 * g.V;
+  g.ndim = ndim;
+  g.n = lx * ly * lz;
+  if (ndim == 1) {
+    g.ok = g.n < (1ull << 32) && (elem_bytes == 4 || elem_bytes == 8);
+    if (!g.ok) return g;
+    g.brick_elems = (uint32_t)g.W * 64;
+    g.nbricks = (uint32_t)((g.n + g.brick_elems - 1) / g.brick_elems);
+    g.nbx = g.nbricks, g.nby = 1, g.nbz = 1;
+    g.nchunks = (uint32_t)((g.n + g.W - 1) / g.W);
+    return g;
+  }
   g.ok = ndim == 3 && lx % (size_t)g.W == 0 && lx * ly * lz < (1ull << 32) && (elem_bytes == 4 || elem_bytes == 8) &&
          8 * lx * ly * (size_t)elem_bytes < (1ull << 31);  // 32-bit buffer offsets within 8 planes
   if (!g.ok) return g;
@@ -1068,11 +1422,11 @@ int brick_configure(BrickLaunch& L, int elem_bytes, int device)
   hipError_t e1, e2;
   if (elem_bytes == 8) {
     e1 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_scan, k_brick3_scan<double, 4, false>, 64 * kBrickWaves, lds_scan);
-    e2 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_pack, k_brick3_pack<4>, 64 * kBrickWaves, lds_pack);
+    e2 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_pack, k_brick3_pack<4, 3>, 64 * kBrickWaves, lds_pack);
   }
   else {
     e1 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_scan, k_brick3_scan<float, 4, false>, 64 * kBrickWaves, lds_scan);
-    e2 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_pack, k_brick3_pack<4>, 64 * kBrickWaves, lds_pack);
+    e2 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_pack, k_brick3_pack<4, 3>, 64 * kBrickWaves, lds_pack);
   }
   if (e1 != hipSuccess || per_scan < 1) per_scan = 1;
   if (e2 != hipSuccess || per_pack < 1) per_pack = 1;
@@ -1093,6 +1447,15 @@ int launch_brick_scan(const BrickLaunch& L, const T* in, double eb, int radius, 
   const BrickGeom& g = L.g;
   const size_t lds = (size_t)(1 + kBrickWaves * kHistCopies) * kMaxBklen * 4;
   const int grid = L.grid_scan;
+  if (g.ndim == 1) {
+    if (zz)
+      k_brick1_scan<T, 4, true><<<grid, 64 * kBrickWaves, lds, st>>>(in, g.n, ebx2_r, r, ol, hist, bhist, bcodes, bklen,
+                                                                     g.nbricks);
+    else
+      k_brick1_scan<T, 4, false><<<grid, 64 * kBrickWaves, lds, st>>>(in, g.n, ebx2_r, r, ol, hist, bhist, bcodes,
+                                                                      bklen, g.nbricks);
+    return (int)hipGetLastError();
+  }
   if (zz)
     k_brick3_scan<T, 4, true><<<grid, 64 * kBrickWaves, lds, st>>>(in, L.lx, L.ly, L.lz, ebx2_r, r, ol, hist, bhist,
                                                                    bcodes, bklen, g.nbx, g.nby, g.nbricks);
@@ -1122,9 +1485,14 @@ int launch_brick_pack(const BrickLaunch& L, const BrickCodes& bcodes, const uint
 {
   const BrickGeom& g = L.g;
   const size_t lds = ((size_t)kMaxBklen + (size_t)kBrickWaves * pack_cells_words<4>()) * 4;
-  k_brick3_pack<4><<<L.grid_pack, 64 * kBrickWaves, lds, st>>>(bcodes, L.ly, L.lz, book, bklen, plan, par_nbit,
-                                                               par_entry, bitstream, g.nbx, g.nby, g.nbricks, reverse,
-                                                               overflow);
+  if (g.ndim == 1)
+    k_brick3_pack<4, 1><<<L.grid_pack, 64 * kBrickWaves, lds, st>>>(bcodes, L.ly, L.lz, book, bklen, plan, par_nbit,
+                                                                    par_entry, bitstream, g.nbx, g.nby, g.nbricks,
+                                                                    reverse, overflow);
+  else
+    k_brick3_pack<4, 3><<<L.grid_pack, 64 * kBrickWaves, lds, st>>>(bcodes, L.ly, L.lz, book, bklen, plan, par_nbit,
+                                                                    par_entry, bitstream, g.nbx, g.nby, g.nbricks,
+                                                                    reverse, overflow);
   return (int)hipGetLastError();
 }
 
@@ -1148,6 +1516,26 @@ int launch_brick_decode(const BrickLaunch& L, const uint32_t* bitstream, size_t 
   const BrickGeom& g = L.g;
   static_assert(sizeof(hfd::LdsTables<kDecB>) + kDecWaves * kDecWaveBytes <= 160 * 1024, "LDS");
   if (bs_words >= (1ull << 30)) return (int)hipErrorInvalidValue;
+  if (g.ndim == 1) {
+    const uint32_t ntiles = (uint32_t)((g.n + 1023) / 1024), nunits = (ntiles + 63) / 64;
+    // waves per CU: the static unit assignment ends when the busiest wave's units are done, and
+    // the CU is throughput-bound, so minimise rounds x waves (ties: more waves)
+    int wpb = 4;
+    size_t best = ~(size_t)0;
+    for (int w = 4; w <= kD1MaxWaves && w <= kDecWaves; w++) {
+      const size_t rounds = (nunits + (size_t)L.ncu * w - 1) / ((size_t)L.ncu * w);
+      if (rounds * w <= best) best = rounds * w, wpb = w;
+    }
+    const uint32_t grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(L.ncu, (nunits + wpb - 1) / wpb));
+    const size_t lds1 = (size_t)wpb * kD1WaveBytes;
+    if (zz)
+      k_brick1_decode<T, true><<<grid, 64 * wpb, lds1, st>>>(bitstream, (uint32_t)bs_words, revbook, bklen, par_nbit,
+                                                             par_entry, out, g.n, ebx2, r, g.nchunks, nunits, ol);
+    else
+      k_brick1_decode<T, false><<<grid, 64 * wpb, lds1, st>>>(bitstream, (uint32_t)bs_words, revbook, bklen, par_nbit,
+                                                              par_entry, out, g.n, ebx2, r, g.nchunks, nunits, ol);
+    return (int)hipGetLastError();
+  }
   // buffer stores address a brick block with 32-bit offsets from its first element
   const size_t plane = (size_t)L.lx * L.ly;
   const bool buf = (7 * plane + 7 * (size_t)L.lx + (size_t)kBlk) * sizeof(T) < (1ull << 31);

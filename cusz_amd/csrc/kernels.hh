@@ -33,8 +33,9 @@ struct X1dOutliers {
   const uint32_t* unsorted = nullptr;  // == epoch: unsorted (the flag word is never reset)
   uint32_t epoch = 0;
 };
+// bstart over units of 2^ushift elements (16384: the 1-D reconstruction; 256: 1-D brick chunks)
 int launch_x1d_bounds(const uint32_t* cells, size_t ncell, size_t n, uint32_t nbricks, uint32_t* bstart,
-                      uint32_t* unsorted, uint32_t epoch, hipStream_t st);
+                      uint32_t* unsorted, uint32_t epoch, hipStream_t st, uint32_t ushift = 14);
 
 template <typename T>
 int launch_lorenzo_x(const uint16_t* codes, T* out, size_t lx, size_t ly, size_t lz, double eb, int radius,
@@ -183,13 +184,16 @@ size_t spline_x_scratch_words(uint32_t ntiles, size_t ncell);
 
 // ---- fused brick pipeline (brick.hip) --------------------------------------------------------
 // A wave owns a W x 8 x 8 brick (W = 64 V); the Huffman chunk length equals W so each brick row
-// is one chunk.  Eligible: 3-D, lx % W == 0.
+// is one chunk.  Eligible: 3-D with lx % W == 0, and 1-D (a brick = 64 consecutive chunks, 16
+// tiles of 1024; the last brick and chunk may be short).
 struct BrickGeom {
   bool ok;
+  int ndim;
   int V, W;
   uint32_t nbx, nby, nbz, nbricks;
   uint32_t brick_elems;
   uint32_t nchunks;
+  size_t n;
 };
 BrickGeom brick_geom(int ndim, size_t lx, size_t ly, size_t lz, int elem_bytes);
 
@@ -238,6 +242,9 @@ struct BrickPlanArgs {
   CompressInfo* info;         // totals; info->pad[0] = block ticket (zeroed per call)
   uint8_t* archive;
   size_t phf_offset, bitstream_rel;
+  uint32_t nd = 3;       // 1: 1-D bricks (64 consecutive chunks; the last chunk may be short)
+  uint32_t nchunks = 0;  // 1-D: chunks of the field
+  size_t n = 0;          // 1-D: elements of the field
 };
 uint32_t brick_units(uint32_t nbricks);
 uint32_t brick_plan_blocks(uint32_t nbricks);

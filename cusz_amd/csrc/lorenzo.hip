@@ -495,16 +495,16 @@ k_scatter(const uint32_t* __restrict__ cells, size_t nnz, T* out, size_t n, cons
 // (every bstart entry is written when the cells are sorted; *unsorted = epoch otherwise)
 __global__ void __launch_bounds__(256) k_x1d_bounds(const uint32_t* __restrict__ cells, size_t ncell, size_t n,
                                                     uint32_t nbricks, uint32_t* bstart, uint32_t* unsorted,
-                                                    uint32_t epoch)
+                                                    uint32_t epoch, uint32_t ushift)
 {
   for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < ncell; i += (size_t)gridDim.x * 256) {
     const uint32_t idx = cells[2 * i + 1];
-    const int64_t b = idx < n ? (int64_t)(idx / 16384) : (int64_t)nbricks;
+    const int64_t b = idx < n ? (int64_t)(idx >> ushift) : (int64_t)nbricks;
     int64_t bp = -1;
     if (i > 0) {
       const uint32_t ip = cells[2 * i - 1];
       if (ip >= idx) *unsorted = epoch;
-      bp = ip < n ? (int64_t)(ip / 16384) : (int64_t)nbricks;
+      bp = ip < n ? (int64_t)(ip >> ushift) : (int64_t)nbricks;
     }
     if (idx >= n) *unsorted = epoch;
     for (int64_t u = bp + 1; u <= b && u <= (int64_t)nbricks; u++) bstart[u] = (uint32_t)i;
@@ -626,12 +626,12 @@ int launch_scatter(const uint32_t* cells, size_t nnz, T* out, size_t n, hipStrea
 }
 
 int launch_x1d_bounds(const uint32_t* cells, size_t ncell, size_t n, uint32_t nbricks, uint32_t* bstart,
-                      uint32_t* unsorted, uint32_t epoch, hipStream_t st)
+                      uint32_t* unsorted, uint32_t epoch, hipStream_t st, uint32_t ushift)
 {
   if (ncell == 0) return 0;
   uint32_t grid = cdiv(ncell, 256);
   if (grid > 4096) grid = 4096;
-  k_x1d_bounds<<<grid, 256, 0, st>>>(cells, ncell, n, nbricks, bstart, unsorted, epoch);
+  k_x1d_bounds<<<grid, 256, 0, st>>>(cells, ncell, n, nbricks, bstart, unsorted, epoch, ushift);
   return (int)hipGetLastError();
 }
 

@@ -198,8 +198,10 @@ struct Pipeline {
     tune_chunking(n, device, &sublen, &pardeg);
     geom = lorenzo_geom(ndim, l.x, l.y, l.z, elem_bytes);
     if (ndim == 1) {
-      CUSZ_AMD_HIP_CHECK(hipMalloc(&d_x1d, ((size_t)geom.nbricks + 2) * 4));
-      CUSZ_AMD_HIP_CHECK(hipMemset(d_x1d, 0, ((size_t)geom.nbricks + 2) * 4));  // unsorted word: no epoch yet
+      // per-unit first cell + unsorted word: units of 16384 (reconstruction) or 256 (brick chunks)
+      const size_t units = std::max<size_t>(geom.nbricks, (n + 255) / 256);
+      CUSZ_AMD_HIP_CHECK(hipMalloc(&d_x1d, (units + 2) * 4));
+      CUSZ_AMD_HIP_CHECK(hipMemset(d_x1d, 0, (units + 2) * 4));  // unsorted word: no epoch yet
     }
     sgeom = spline_geom(l.x, l.y, l.z);
     spl_cap = (uint32_t)(std::min<size_t>(l.x, 32) * std::min<size_t>(l.y, 8) * std::min<size_t>(l.z, 8) / 10 + 16);
@@ -564,6 +566,7 @@ struct Pipeline {
     BrickPlanArgs pa{d_bhist, bklen, brick_hist_stride(bklen), d_book, g.nbricks, brick_units(g.nbricks), g.nbx, g.nby, bl.ly, bl.lz,
                      d_brick_cnt, cap, d_slots, d_spill, spill_cnt(), spill_cap, nblk, d_ub, d_bbase, d_brick_off,
                      d_plan, d_plan + nblk + 1, info(), d_archive, phf_off, bits_rel};
+    pa.nd = (uint32_t)g.ndim, pa.nchunks = g.nchunks, pa.n = g.n;
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_plan(bl, pa, h, &ph, stream));
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_pack(bl, brick_codes(pend.zz, radius), d_book, bklen, pa, par_nbit, par_entry, bits,
                                                      pack_reverse, timeout(), stream));
@@ -662,9 +665,14 @@ struct Pipeline {
     // they are grouped and sorted; only otherwise does the scatter below run (only_if = unsorted)
     BrickOutliers bo;
     if (brickdec && !zz && h->splen) {
-      const uint32_t nb = bl.g.nbricks;
-      CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_cell_bounds(bl, cells, h->splen, d_x1d, d_x1d + nb + 1,
-                                                              next_cell_epoch(), stream));
+      // cells per brick (3-D) or per chunk (1-D)
+      const uint32_t nb = bl.g.ndim == 1 ? bl.g.nchunks : bl.g.nbricks;
+      if (bl.g.ndim == 1)
+        CUSZ_AMD_HIP_CHECK((hipError_t)launch_x1d_bounds(cells, h->splen, n, nb, d_x1d, d_x1d + nb + 1,
+                                                         next_cell_epoch(), stream, 8));
+      else
+        CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_cell_bounds(bl, cells, h->splen, d_x1d, d_x1d + nb + 1,
+                                                                next_cell_epoch(), stream));
       bo = BrickOutliers{cells, (size_t)h->splen, d_x1d, d_x1d + nb + 1, cell_epoch};
       ox.unsorted = bo.unsorted;
       ox.epoch = cell_epoch;

@@ -15,7 +15,8 @@ import cusz_amd as cz  # noqa: E402
 from cusz_amd import datagen  # noqa: E402
 
 dims = tuple(int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "512x512x512").split("x"))
-x = datagen.smooth3d_torch(dims, seed=2, device="cuda")
+x = (datagen.hacc1d_torch(dims[0], seed=3) if dims[1] == dims[2] == 1 else
+     datagen.smooth3d_torch(dims, seed=2, device="cuda"))
 y = torch.empty_like(x)
 s = torch.cuda.current_stream()
 r = cz.Resource(cz.F4, dims, stream=s.cuda_stream)
@@ -35,9 +36,9 @@ torch.cuda.synchronize()
 L.psz_amd_debug_brick_profile(buf, 1)
 v = [buf[i] / reps for i in range(16)]
 nbk = v[0]
-print(f"decompress {ev[0].elapsed_time(ev[1]) / reps * 1e3:.1f} us per call (profiled build), bricks {nbk:.0f}")
+print(f"decompress {ev[0].elapsed_time(ev[1]) / reps * 1e3:.1f} us per call (profiled build), bricks (1-D: unit phases) {nbk:.0f}")
 for i, nm in [(1, "start"), (2, "decode"), (3, "drain"), (4, "recon")]:
     print(f"  {nm:7s} {v[i] / nbk:10.0f} cycles/brick")
-print(f"  loop iterations {v[5] / nbk:.1f}/brick ({v[5] / nbk * 2 * 8:.0f} steps)")
+print(f"  loop iterations {v[5] / nbk:.1f}/brick ({v[5] / nbk * 2 * 4:.0f} wave-steps, kF = 4)")
 print(f"  lane-steps: done {v[7] / nbk:.0f}/brick, starved {v[6] / nbk:.0f}/brick")
 print(f"max err {(y.double() - x.double()).abs().max().item():.3e}")

@@ -32,6 +32,17 @@ CASES = [
     ((256, 16, 16), np.float32, 1e-2, True, 512, "noise"),     # and pass-1 byte codes escaping to u16
     ((256, 16, 16), np.float64, 3e-2, False, 256, "noise"),
     ((256, 16, 8), np.float32, 0.5, False, 512, "int"),
+    # 1-D bricks: 64 chunks of 256; units of 64 tiles of 1024 in the decoder (ragged ends)
+    ((16384, 1, 1), np.float32, 1e-4, False, 512, "smooth"),
+    ((100_003, 1, 1), np.float32, 1e-4, False, 512, "hacc"),
+    ((65536 * 3 + 1000, 1, 1), np.float32, 1e-3, False, 512, "hacc"),
+    ((300, 1, 1), np.float32, 1e-4, False, 512, "smooth"),
+    ((100_003, 1, 1), np.float64, 1e-4, False, 512, "hacc"),
+    ((70_001, 1, 1), np.float32, 1e-4, True, 512, "hacc"),
+    ((70_001, 1, 1), np.float64, 1e-4, True, 512, "hacc"),
+    ((50_000, 1, 1), np.float32, 1e-2, False, 512, "noise"),
+    ((50_000, 1, 1), np.float32, 1e-3, False, 64, "hacc"),     # many outliers per block row
+    ((40_000, 1, 1), np.float32, 0.5, False, 512, "int"),
 ]
 
 
@@ -42,6 +53,8 @@ def _field(kind, dims, dtype, seed):
         return datagen.smooth3d_np(dims, seed, dtype=dtype)
     if kind == "noise":
         return rng.standard_normal(n).astype(dtype)
+    if kind == "hacc":
+        return datagen.hacc1d_np(n, seed).astype(dtype)
     return np.cumsum(rng.integers(-3, 4, n)).astype(dtype)
 
 

@@ -1,7 +1,9 @@
-"""1-D Lorenzo reconstruction reading the outlier values straight from the archive's cells
-(lorenzo.hip k_lorenzo_x1d with X1dOutliers): sorted cells (no spill) take that path, cells with
-a spill tail (one brick over its slot) fall back to the scatter.  Both must equal the oracle's
-decompression bit for bit (run_roundtrip), and a shuffled cell list must decompress identically.
+"""1-D reconstruction reading the outlier values straight from the archive's cells: the
+reference layout's k_lorenzo_x1d (X1dOutliers, per 16384-element brick) and the fused 1-D brick
+decoder (brick.hip k_brick1_decode, per chunk).  Sorted cells (no spill) take that path, cells
+with a spill tail (one brick over its slot) fall back to the scatter.  Both must equal the
+oracle's decompression bit for bit (run_roundtrip), and a shuffled cell list must decompress
+identically.
 """
 import numpy as np
 import pytest
@@ -25,19 +27,25 @@ def _walk(n, seed, jump_frac=0.05, burst=None):
     return x
 
 
+LAYOUTS = [cz.LAYOUT_BRICK, cz.LAYOUT_REFERENCE]
+
+
+@pytest.mark.parametrize("layout", LAYOUTS, ids=["brick", "reference"])
 @pytest.mark.parametrize("n,burst", [(300_001, None), (16384 * 3 + 77, None), (200_000, (40_000, 50_000)),
                                      (16384, None)])
-def test_x1d_outliers_match_oracle(oracle, n, burst):
+def test_x1d_outliers_match_oracle(oracle, n, burst, layout):
     data = _walk(n, n, burst=burst)
-    run_roundtrip(oracle, data, (n, 1, 1), 0.05)
+    run_roundtrip(oracle, data, (n, 1, 1), 0.05, layout=layout)
 
 
-def test_x1d_shuffled_cells_decompress_identically():
+@pytest.mark.parametrize("layout", LAYOUTS, ids=["brick", "reference"])
+def test_x1d_shuffled_cells_decompress_identically(layout):
     import torch
 
     n = 100_000
     data = _walk(n, 7)
     r = cz.Resource(cz.F4, (n, 1, 1))
+    r.set_layout(layout)
     d_in = to_device(data)
     ptr, nbytes, _ = r.compress(d_in.data_ptr(), 0.05, cz.Abs)
     arch = bytearray(d2h(ptr, nbytes).tobytes())
