@@ -27,6 +27,7 @@
 // reads chunk c from there, hf_kernels.cuhip.inl:386-391); chunks are laid out brick by brick,
 // and the few cells between a brick's last chunk and the next region are zero.
 #include <algorithm>
+#include <type_traits>
 
 #include "archive_device.hh"
 #include "common.hh"
@@ -816,6 +817,17 @@ __device__ __forceinline__ void buf_store<double>(double v, __amdgpu_buffer_rsrc
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, (int)voff, (int)soff, 0);
 }
 
+// four consecutive elements (16 B for f32, 32 B for f64) at byte offset voff
+template <typename T>
+__device__ __forceinline__ void buf_store4(const T* v, __amdgpu_buffer_rsrc_t r, uint32_t voff)
+{
+  typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+  u32x4v w[sizeof(T) / 4];
+  __builtin_memcpy(&w[0], v, 4 * sizeof(T));
+#pragma unroll
+  for (int i = 0; i < (int)sizeof(T) / 4; i++) __builtin_amdgcn_raw_buffer_store_b128(w[i], r, (int)(voff + 16 * i), 0, 0);
+}
+
 // Outlier values of one brick for the reconstruction, without the scatter pass: the archive's
 // cells of the brick are contiguous and sorted by (row, x) (this compressor writes them so; a
 // bounds pass checks it), so the k-th zero code of a row, in x order, takes the row's k-th cell.
@@ -1188,30 +1200,24 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
 }
 // ---- 1-D: fused decode + reconstruct -------------------------------------------------------
 // A wave owns a unit of 64 tiles of 1024 (4 chunks of 256 each); lane l owns tile 64 u + l and
-// decodes its four chunks in four phases (phase p: chunk 4 t + p), so a reconstruction block
-// holds, for every tile of the unit, the same 64 columns of chunk p.  The reference's 1-D order
-// (lrz_x.cuhip.inl:11-78, wave32.cuhip.inl:7-66: per thread 4 sequential elements, Hillis-Steele
-// over the 32 thread totals of each 128-element segment, then a serial sum of the segment totals)
-// runs per block with lane = (row 4 i + l / 16, group l % 16): a block is half a segment -- the
-// first half's raw thread totals stay in registers for the second half's scan (stages d = 1..8 in
-// DPP rows of 16 lanes, the lanes below d reading the first half by row_ror), and the serial
-// segment carry of each tile stays in registers across the phases.
+// decodes its four chunks in four phases (phase p: chunk 4 t + p).  After each block of 64
+// columns the lane reconstructs its own row -- 16 reference threads of 4 elements -- in
+// registers, in the reference's 1-D order (lrz_x.cuhip.inl:11-78, wave32.cuhip.inl:7-66): per
+// thread 4 sequential sums; Hillis-Steele over the 32 thread totals of each 128-element segment
+// (a block is half a segment: the first half's raw totals stay in registers for the second
+// half, which runs the 32-wide scan); a serial sum of the segment totals, carried per tile
+// across the phases.  No cross-lane traffic; the lane stores its 256-B row piece.
 //
 // Outliers (archive cells in index order, k_x1d_bounds with chunk granularity): each lane
 // prefetches the next kCellPf cell values of its chunk at a block's start (they land while the
-// block decodes) and the reconstruction ranks each row's zero codes against them; ranks past the
-// prefetch read the cell directly.
+// block decodes, and go to LDS for the reconstruction); zero codes take them by rank, ranks past
+// the prefetch read the cell directly.
 constexpr uint32_t kCellPf = 8;
-constexpr size_t kD1Cur = kDecTile + (size_t)64 * kTP * 2;  // cursor[64] | end[64] | values[64][kCellPf]
-constexpr size_t kD1WaveBytes = kD1Cur + (size_t)(2 * 64 + 64 * kCellPf) * 4;
-constexpr int kD1MaxWaves = (int)((160 * 1024 - sizeof(hfd::LdsTables<kDecB>)) / kD1WaveBytes);
+constexpr uint32_t kCvPitch = kCellPf + 1;  // odd word pitch: lane rows on distinct banks
+constexpr size_t kD1Cv = kDecTile + (size_t)64 * kTP * 2;  // values[64][kCvPitch]
+constexpr size_t kD1WaveBytes = kD1Cv + (size_t)64 * kCvPitch * 4;
+constexpr int kD1MaxWaves = (int)((160 * 1024 - sizeof(hfd::LdsTables<kDecB>) - 512) / kD1WaveBytes);
 static_assert(kD1MaxWaves >= 4, "LDS");
-
-template <int CTRL, typename T>
-__device__ __forceinline__ T dpp16(T v)  // DPP row op within 16-lane rows; lanes without a source read 0
-{
-  return dppf<CTRL, 0xf>(v);
-}
 
 template <typename T, bool ZZ>
 __global__ void __launch_bounds__(64 * kDecWaves)
@@ -1226,9 +1232,7 @@ k_brick1_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* wbase = dsm + (size_t)wid * kD1WaveBytes;
   uint16_t* tile = reinterpret_cast<uint16_t*>(wbase + kDecTile);
-  uint32_t* cur = reinterpret_cast<uint32_t*>(wbase + kD1Cur);  // next cell of each row's chunk
-  uint32_t* cend = cur + 64;
-  uint32_t* cvals = cend + 64;
+  uint32_t* cv = reinterpret_cast<uint32_t*>(wbase + kD1Cv) + lane * kCvPitch;  // this lane's values
   const bool ranked = !ZZ && (ol.ncell == 0 || *ol.unsorted != ol.epoch);  // else: values in `out` (scatter)
   const uint32_t npf = ol.ncell < (1u << 28) ? kCellPf : 0u;  // prefetched ranks (32-bit buffer offsets)
   const DecWave dw{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(bitstream), 0, (int)(bs_words * 4u), (int)kBufRsrcW3),
@@ -1236,14 +1240,15 @@ k_brick1_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
   const __amdgpu_buffer_rsrc_t rcells = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint32_t*>(ol.cells), 0, (int)min(ol.ncell * 8, (size_t)0x7FFFFFFF), (int)kBufRsrcW3);
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
-  const uint32_t g = (uint32_t)lane & 15u, rsub = (uint32_t)lane >> 4;
-  const uint64_t rowbits = 0xFFFFull << (lane & 48), lt = (1ull << lane) - 1ull;
   BPROF(unsigned long long pc[8] = {}; unsigned long long tk = __builtin_readcyclecounter(), tp = tk;)
   for (uint32_t u = blockIdx.x * (blockDim.x >> 6) + wid; u < nunits; u += nw) {
-    T carr[16], fh[16];  // per recon row 4 i + rsub: tile carry; first-half raw totals
-#pragma unroll
-    for (int i = 0; i < 16; i++) carr[i] = T(0);
-    const bool full = (size_t)(u + 1) * 65536u <= n;  // every element of the unit is in the field
+    T carry = T(0);  // serial sum of this tile's segment totals (exclusive)
+    T fh[16];        // raw thread totals of the current segment's first half
+    const size_t ubase = (size_t)u * 65536u;
+    const bool full = ubase + 65536u <= n;  // every element of the unit is in the field (uniform)
+    // unit-relative stores: 32-bit offsets; past the field's end they are dropped
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        out + ubase, 0, (int)(min((size_t)65536u, n - ubase) * sizeof(T)), (int)kBufRsrcW3);
     for (uint32_t p = 0; p < 4; p++) {
       BPROF(pc[0]++; tp = __builtin_readcyclecounter();)
       const size_t c = ((size_t)u * 64u + (uint32_t)lane) * 4u + p;
@@ -1251,122 +1256,139 @@ k_brick1_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
       const uint32_t nbit = live ? par_nbit[c] : 0u;
       const uint32_t vbase = (live ? par_entry[c] : 0u) * 4u;
       const uint32_t vlen = live ? (uint32_t)min((size_t)256, n - c * 256u) : 0u;
+      uint32_t cur = 0, cend = 0;  // this chunk's cells [cur, cend), cur advancing
       u32x4 pf[kCellPf / 2];
       auto pro = [&]() {
-        if (!ranked) return;
-        cur[lane] = live && ol.ncell ? ol.bstart[c] : 0u;
-        cend[lane] = live && ol.ncell ? ol.bstart[c + 1] : 0u;
+        if (ranked && live && ol.ncell) cur = ol.bstart[c], cend = ol.bstart[c + 1];
       };
       auto blk_start = [&](int) {
         if (!ranked) return;
-        const uint32_t cb = cur[lane];
 #pragma unroll
         for (int h = 0; h < (int)kCellPf / 2; h++)
-          pf[h] = __builtin_amdgcn_raw_buffer_load_b128(rcells, (int)(live && npf ? cb * 8u + 16u * h : kOOB), 0, 0);
+          pf[h] = __builtin_amdgcn_raw_buffer_load_b128(rcells, (int)(live && npf ? cur * 8u + 16u * h : kOOB), 0, 0);
       };
       auto recon = [&](int blk) {
-        if (ranked) {
+        const uint32_t roff = ((uint32_t)lane * 1024u + p * 256u + (uint32_t)blk * kBlk) * (uint32_t)sizeof(T);
+        const uint32_t* trow = reinterpret_cast<const uint32_t*>(tile + lane * kTP);
+        if (ranked) {  // the prefetched values; ranks at or past the chunk's last cell read 0
 #pragma unroll
           for (int h = 0; h < (int)kCellPf / 2; h++) {
-            cvals[lane * kCellPf + 2 * h] = pf[h].x;
-            cvals[lane * kCellPf + 2 * h + 1] = pf[h].z;
+            cv[2 * h] = cur + 2u * h < cend ? pf[h].x : 0u;
+            cv[2 * h + 1] = cur + 2u * h + 1u < cend ? pf[h].z : 0u;
           }
-          hfd::wave_sync();
         }
-        const bool odd = blk & 1;
+        T v[64];
+        uint32_t tw[32];  // the row's 64 codes, all read before use (one LDS wait)
 #pragma unroll
-        for (int i = 0; i < 16; i++) {
-          const uint32_t R = 4u * i + rsub;
-          const uint32_t* tr = reinterpret_cast<const uint32_t*>(tile + R * kTP) + 2 * g;
-          const uint32_t c01 = tr[0], c23 = tr[1];
-          const uint32_t cd[4] = {c01 & 0xFFFFu, c01 >> 16, c23 & 0xFFFFu, c23 >> 16};
-          const size_t e0 = (((size_t)u * 64u + R) * 4u + p) * 256u + (uint32_t)blk * kBlk + 4u * g;
-          T v[4];
+        for (int q = 0; q < 32; q++) tw[q] = trow[q];
+        uint32_t rk = 0;  // zero codes so far in this block
+        // values of the codes: (o + c) - r, where a zero code's o is its cell by rank and any other
+        // code's o is 0 -- one of the two is zero, so the sum is the other exactly and the value is
+        // (z ? o : c) - r.  The rank's value is read for every code and selected bitwise, so no
+        // code branches.
+        auto values = [&](auto rtag) {
+          constexpr bool RK = decltype(rtag)::value;
 #pragma unroll
-          for (int k = 0; k < 4; k++) v[k] = ZZ ? (T)zz_dec((uint16_t)cd[k]) : (T)cd[k] - r;
-          if (ranked) {
-            bool z[4];
-            uint64_t m[4];
-            uint32_t below = 0, tot = 0;
+          for (int q = 0; q < 32; q++)
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-              z[k] = cd[k] == 0u;
-              m[k] = __builtin_amdgcn_ballot_w64(z[k]);
-              below += (uint32_t)__builtin_popcountll(m[k] & rowbits & lt);
-              tot += (uint32_t)__builtin_popcountll(m[k] & rowbits);
-            }
-            if (m[0] | m[1] | m[2] | m[3]) {
-              const uint32_t cb = cur[R], ce = cend[R];
-              uint32_t rk = below;
-#pragma unroll
-              for (int k = 0; k < 4; k++) {
-                if (z[k]) {
-                  const uint32_t j = cb + rk;
-                  T o = T(0);
-                  if (j < ce) o = (T)__builtin_bit_cast(float, rk < npf ? cvals[R * kCellPf + rk] : ol.cells[2 * (size_t)j]);
-                  v[k] = o - r;  // (o + 0) - r
-                  rk++;
-                }
+            for (int h = 0; h < 2; h++) {
+              const uint32_t cd = h ? tw[q] >> 16 : tw[q] & 0xFFFFu;
+              T x;
+              if constexpr (ZZ)
+                x = (T)zz_dec((uint16_t)cd);
+              else if constexpr (RK) {
+                const uint32_t zm = 0u - (uint32_t)(cd == 0u);  // all ones for a zero code
+                const uint32_t val = cv[rk];  // ranks past the prefetch: fixed below (reads stay in LDS)
+                const float cf = (float)cd;     // exact (codes < 2^16)
+                const uint32_t b = (val & zm) | (__builtin_bit_cast(uint32_t, cf) & ~zm);
+                x = (T)__builtin_bit_cast(float, b) - r;
+                rk -= zm;  // + 1 for a zero code
               }
-              hfd::wave_sync();
-              if (g == 0) cur[R] = cb + tot;
+              else
+                x = (T)cd - r;
+              v[2 * q + h] = x;
+            }
+        };
+        if (ranked)
+          values(std::true_type{});
+        else
+          values(std::false_type{});
+        if (ranked && __builtin_amdgcn_ballot_w64(rk > npf)) {  // ranks past the prefetch (rare)
+          uint32_t j = 0;
+#pragma unroll
+          for (int q = 0; q < 32; q++) {
+            const uint32_t w = tw[q];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+              const bool z = (h ? w >> 16 : w & 0xFFFFu) == 0u;
+              if (z && j >= npf)
+                v[2 * q + h] = (cur + j < cend ? (T)__builtin_bit_cast(float, ol.cells[2 * (size_t)(cur + j)]) : T(0)) - r;
+              j += z ? 1u : 0u;
             }
           }
-          else if (__builtin_amdgcn_ballot_w64(cd[0] == 0u || cd[1] == 0u || cd[2] == 0u || cd[3] == 0u)) {
+        }
+        if (ranked) cur += rk;
+        if (!ranked) {  // values scattered into `out`: plane + zz_dec(0), or (plane + 0) - r
 #pragma unroll
-            for (int k = 0; k < 4; k++)
-              if (cd[k] == 0u) {
-                const T o = (full || e0 + k < n) ? out[e0 + k] : T(0);
-                v[k] = ZZ ? o + v[k] : o - r;  // plane + zz_dec(0), or (plane + 0) - r
+          for (int q = 0; q < 32; q++) {
+            const uint32_t w = tw[q];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+              if ((h ? w >> 16 : w & 0xFFFFu) == 0u) {
+                const uint32_t off = roff + (uint32_t)(2 * q + h) * (uint32_t)sizeof(T);
+                T o;
+                if constexpr (sizeof(T) == 4)
+                  o = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(ro, (int)off, 0, 0));
+                else
+                  o = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(ro, (int)off, 0, 0));
+                v[2 * q + h] = ZZ ? o + v[2 * q + h] : o - r;
               }
+            }
           }
-          // per thread: 4 sequential elements (wave32.cuhip.inl:10)
-          v[1] = v[1] + v[0];
-          v[2] = v[2] + v[1];
-          v[3] = v[3] + v[2];
-          // thread totals: Hillis-Steele over the segment's 32 (wave32.cuhip.inl:14-17)
-          T prev;
-          if (!odd) {
-            T a = v[3];
-            fh[i] = a;
-            a = a + dpp16<0x111>(a);
-            a = a + dpp16<0x112>(a);
-            a = a + dpp16<0x114>(a);
-            a = a + dpp16<0x118>(a);
-            prev = dpp16<0x111>(a);  // group 0 of the segment adds nothing
-          }
-          else {
-            // group 16 + g reads group 16 + g - d: lane g - d of b, or lane g - d + 16 of f.  The
-            // choice is made on the source side (lane s < 16 - d offers b, the others f) so the
-            // DPP rotate runs with every lane active (a select of two DPP results may be turned
-            // into a branch, and a DPP under a partial exec mask reads 0 from inactive lanes)
-            T f = fh[i], b = v[3];
-#define D1_STAGE(D)                                                                   \
-  {                                                                                   \
-    const T bs = dpp16<0x120 + (D)>(g < 16u - (D) ? b : f);                           \
-    f = f + dpp16<0x110 + (D)>(f);                                                    \
-    b = b + bs;                                                                       \
-  }
-            D1_STAGE(1) D1_STAGE(2) D1_STAGE(4) D1_STAGE(8)
-#undef D1_STAGE
-            b = b + f;  // d = 16: group 16 + g adds group g
-            prev = dpp16<0x121>(g == 15u ? f : b);  // group 15 + g: f[15] for g = 0, else b[g - 1]
-          }
+        }
+        // per thread: 4 sequential elements (wave32.cuhip.inl:10)
 #pragma unroll
-          for (int k = 0; k < 4; k++) v[k] = v[k] + prev;
-          // serial sum of the segment totals (wave32.cuhip.inl:38-42): this segment's carry
-          const T cin = carr[i];
-          if (odd) carr[i] = cin + __shfl(v[3], (lane & 48) | 15);
+        for (int t = 0; t < 16; t++) {
+          v[4 * t + 1] = v[4 * t + 1] + v[4 * t];
+          v[4 * t + 2] = v[4 * t + 2] + v[4 * t + 1];
+          v[4 * t + 3] = v[4 * t + 3] + v[4 * t + 2];
+        }
+        // thread totals: Hillis-Steele over the segment's 32 (wave32.cuhip.inl:14-17), descending
+        // in place (each stage reads the previous stage's values); a[t] then holds thread t's
+        // inclusive total and thread t adds a[t - 1]
+        T a[32];
+        const int t0 = (blk & 1) ? 16 : 0;  // this block's threads are t0 .. t0 + 15
+#pragma unroll
+        for (int t = 0; t < 16; t++) {
+          if (blk & 1) a[t] = fh[t];
+          a[t0 + t] = v[4 * t + 3];
+          if (!(blk & 1)) fh[t] = v[4 * t + 3];
+        }
+        const int nt = t0 + 16;
+#pragma unroll
+        for (int d = 1; d < 32; d *= 2)
+#pragma unroll
+          for (int t = 31; t >= d; t--)
+            if (t < nt) a[t] = a[t] + a[t - d];
+        // add the previous thread's total, the segment carry, the scale; store the row piece
+        T tot = T(0);
+#pragma unroll
+        for (int t = 0; t < 16; t++) {
           T o[4];
 #pragma unroll
-          for (int k = 0; k < 4; k++) o[k] = (v[k] + cin) * ebx2;
-          if (full || e0 + 4 <= n)
-            store_row<T, 4>(out, e0, 0, 4, true, o);
+          for (int k = 0; k < 4; k++) {
+            const T pv = (t0 + t > 0) ? v[4 * t + k] + a[t0 + t - 1] : v[4 * t + k];
+            o[k] = (pv + carry) * ebx2;
+            if (k == 3 && t == 15) tot = pv;  // the segment's total (second half)
+          }
+          const uint32_t off = roff + (uint32_t)(4 * t) * (uint32_t)sizeof(T);
+          if (full)
+            buf_store4<T>(o, ro, off);
           else
 #pragma unroll
-            for (int k = 0; k < 4; k++)
-              if (e0 + k < n) out[e0 + k] = o[k];
+            for (int k = 0; k < 4; k++) buf_store<T>(o[k], ro, off + (uint32_t)k * (uint32_t)sizeof(T), 0);
         }
+        if (blk & 1) carry = carry + tot;
       };
       decode_chunks(tb, rg, dw, live, vbase, nbit, vlen, pro, blk_start, recon BPROF_A);
     }
@@ -1526,6 +1548,9 @@ int launch_brick_decode(const BrickLaunch& L, const uint32_t* bitstream, size_t 
       const size_t rounds = (nunits + (size_t)L.ncu * w - 1) / ((size_t)L.ncu * w);
       if (rounds * w <= best) best = rounds * w, wpb = w;
     }
+#ifdef CUSZ_AMD_D1_WAVES  // (experiment: fixed waves per CU)
+    wpb = CUSZ_AMD_D1_WAVES;
+#endif
     const uint32_t grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(L.ncu, (nunits + wpb - 1) / wpb));
     const size_t lds1 = (size_t)wpb * kD1WaveBytes;
     if (zz)

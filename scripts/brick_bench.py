@@ -28,7 +28,10 @@ def main():
     a = ap.parse_args()
     dims = tuple(int(v) for v in a.dims.split("x"))
     dt = torch.float64 if a.f64 else torch.float32
-    d_in = datagen.smooth3d_torch(dims, seed=2, dtype=dt)
+    if dims[1] == dims[2] == 1:  # 1-D: the config-3 recipe
+        d_in = datagen.hacc1d_torch(dims[0], seed=3).to(dt)
+    else:
+        d_in = datagen.smooth3d_torch(dims, seed=2, dtype=dt)
     n = d_in.numel()
     out = torch.empty(n, dtype=dt, device="cuda")
     st = torch.cuda.current_stream()
