@@ -828,6 +828,28 @@ __device__ __forceinline__ void buf_store4(const T* v, __amdgpu_buffer_rsrc_t r,
   for (int i = 0; i < (int)sizeof(T) / 4; i++) __builtin_amdgcn_raw_buffer_store_b128(w[i], r, (int)(voff + 16 * i), 0, 0);
 }
 
+template <typename T>
+__device__ __forceinline__ void lds_store4(T* p, const T (&v)[4])
+{
+  typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int i = 0; i < (int)sizeof(T) / 4; i++) {
+    u32x4v w;
+    __builtin_memcpy(&w, reinterpret_cast<const char*>(&v[0]) + 16 * i, 16);
+    reinterpret_cast<u32x4v*>(p)[i] = w;
+  }
+}
+template <typename T>
+__device__ __forceinline__ void lds_load4(const T* p, T (&v)[4])
+{
+  typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int i = 0; i < (int)sizeof(T) / 4; i++) {
+    const u32x4v w = reinterpret_cast<const u32x4v*>(p)[i];
+    __builtin_memcpy(reinterpret_cast<char*>(&v[0]) + 16 * i, &w, 16);
+  }
+}
+
 // Outlier values of one brick for the reconstruction, without the scatter pass: the archive's
 // cells of the brick are contiguous and sorted by (row, x) (this compressor writes them so; a
 // bounds pass checks it), so the k-th zero code of a row, in x order, takes the row's k-th cell.
@@ -989,7 +1011,7 @@ __global__ void __launch_bounds__(256) k_brick_cell_bounds(const uint32_t* __res
 }
 
 #ifdef CUSZ_AMD_DEC_PROFILE
-#define BPROF_P , unsigned long long(&pc)[8], unsigned long long &tk, unsigned long long &tp
+#define BPROF_P , unsigned long long(&pc)[16], unsigned long long &tk, unsigned long long &tp
 #define BPROF_A , pc, tk, tp
 #else
 #define BPROF_P
@@ -1111,17 +1133,16 @@ __device__ __forceinline__ void decode_chunks(const hfd::LdsTables<kDecB>& tb, c
     consume(pb, fb);
     hfd::wave_sync();
     BPROF(tk = __builtin_readcyclecounter(); pc[3] += tk - tp; tp = tk;)
+    // symbols decoded past the block end move to its front (`keep` carries a pending one); they
+    // are held in registers across the reconstruction, which may use the tile as scratch
+    uint32_t* rw = reinterpret_cast<uint32_t*>(dw.tile + lane * kTP);
+    uint32_t ovs[kF + 1];
+#pragma unroll
+    for (int i = 0; i <= kF; i++) ovs[i] = rw[kBlk / 2 + i];
     recon(blk);
     hfd::wave_sync();
-    // symbols decoded past the block end move to its front (`keep` carries a pending one)
-    {
-      uint32_t* rw = reinterpret_cast<uint32_t*>(dw.tile + lane * kTP);
-      uint32_t v[kF + 1];
 #pragma unroll
-      for (int i = 0; i <= kF; i++) v[i] = rw[kBlk / 2 + i];
-#pragma unroll
-      for (int i = 0; i <= kF; i++) rw[i] = v[i];
-    }
+    for (int i = 0; i <= kF; i++) rw[i] = ovs[i];
     hfd::wave_sync();
     BPROF(tk = __builtin_readcyclecounter(); pc[4] += tk - tp; tp = tk;)
   }
@@ -1151,7 +1172,7 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
   const uint32_t ry = (uint32_t)lane >> 3, rz = (uint32_t)lane & 7u;
 
-  BPROF(unsigned long long pc[8] = {}; unsigned long long tk = __builtin_readcyclecounter(), tp = tk;)
+  BPROF(unsigned long long pc[16] = {}; unsigned long long tk = __builtin_readcyclecounter(), tp = tk;)
   for (uint32_t brick = blockIdx.x * (blockDim.x >> 6) + wid; brick < nbricks; brick += nw) {
     BPROF(pc[0]++; tp = __builtin_readcyclecounter();)
     const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
@@ -1195,7 +1216,7 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
   }
 #ifdef CUSZ_AMD_DEC_PROFILE
   if (lane == 0)
-    for (int i = 0; i < 8; i++) atomicAdd(&g_brick_prof[i], pc[i]);
+    for (int i = 0; i < 16; i++) atomicAdd(&g_brick_prof[i], pc[i]);
 #endif
 }
 // ---- 1-D: fused decode + reconstruct -------------------------------------------------------
@@ -1218,6 +1239,7 @@ constexpr size_t kD1Cv = kDecTile + (size_t)64 * kTP * 2;  // values[64][kCvPitc
 constexpr size_t kD1WaveBytes = kD1Cv + (size_t)64 * kCvPitch * 4;
 constexpr int kD1MaxWaves = (int)((160 * 1024 - sizeof(hfd::LdsTables<kDecB>) - 512) / kD1WaveBytes);
 static_assert(kD1MaxWaves >= 4, "LDS");
+static_assert(64 * 144 <= 64 * kTP * 2, "store staging fits the code tile");
 
 template <typename T, bool ZZ>
 __global__ void __launch_bounds__(64 * kDecWaves)
@@ -1240,7 +1262,7 @@ k_brick1_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
   const __amdgpu_buffer_rsrc_t rcells = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint32_t*>(ol.cells), 0, (int)min(ol.ncell * 8, (size_t)0x7FFFFFFF), (int)kBufRsrcW3);
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
-  BPROF(unsigned long long pc[8] = {}; unsigned long long tk = __builtin_readcyclecounter(), tp = tk;)
+  BPROF(unsigned long long pc[16] = {}; unsigned long long tk = __builtin_readcyclecounter(), tp = tk;)
   for (uint32_t u = blockIdx.x * (blockDim.x >> 6) + wid; u < nunits; u += nw) {
     T carry = T(0);  // serial sum of this tile's segment totals (exclusive)
     T fh[16];        // raw thread totals of the current segment's first half
@@ -1268,6 +1290,9 @@ k_brick1_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
           pf[h] = __builtin_amdgcn_raw_buffer_load_b128(rcells, (int)(live && npf ? cur * 8u + 16u * h : kOOB), 0, 0);
       };
       auto recon = [&](int blk) {
+#ifdef CUSZ_AMD_EXP_NORECON
+        if (blk < 100) return;
+#endif
         const uint32_t roff = ((uint32_t)lane * 1024u + p * 256u + (uint32_t)blk * kBlk) * (uint32_t)sizeof(T);
         const uint32_t* trow = reinterpret_cast<const uint32_t*>(tile + lane * kTP);
         if (ranked) {  // the prefetched values; ranks at or past the chunk's last cell read 0
@@ -1281,26 +1306,46 @@ k_brick1_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
         uint32_t tw[32];  // the row's 64 codes, all read before use (one LDS wait)
 #pragma unroll
         for (int q = 0; q < 32; q++) tw[q] = trow[q];
+#ifdef CUSZ_AMD_EXP_NOTW
+#pragma unroll
+        for (int q = 0; q < 32; q++) tw[q] = (uint32_t)(lane * 7 + q * 3 + blk) & 0x01FF01FFu;
+#endif
         uint32_t rk = 0;  // zero codes so far in this block
         // values of the codes: (o + c) - r, where a zero code's o is its cell by rank and any other
         // code's o is 0 -- one of the two is zero, so the sum is the other exactly and the value is
         // (z ? o : c) - r.  The rank's value is read for every code and selected bitwise, so no
         // code branches.
+        // The value reads are issued 16 at a time (ranks first, then the reads, then the selects):
+        // under the decode's LDS traffic their latency is long, and a wait per code would serialise.
         auto values = [&](auto rtag) {
           constexpr bool RK = decltype(rtag)::value;
 #pragma unroll
-          for (int q = 0; q < 32; q++)
+          for (int s = 0; s < 4; s++) {
+            uint32_t val[16];
+            if constexpr (RK && !ZZ) {
+              uint32_t rr = rk;
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
+              for (int e = 0; e < 16; e++) {
+                const uint32_t cd = (e & 1) ? tw[8 * s + e / 2] >> 16 : tw[8 * s + e / 2] & 0xFFFFu;
+#ifndef CUSZ_AMD_EXP_NOCV
+                val[e] = cv[rr];  // ranks past the prefetch: fixed below (reads stay in LDS)
+#else
+                val[e] = rr;
+#endif
+                rr += cd == 0u ? 1u : 0u;
+              }
+            }
+#pragma unroll
+            for (int e = 0; e < 16; e++) {
+              const int q = 8 * s + e / 2, h = e & 1;
               const uint32_t cd = h ? tw[q] >> 16 : tw[q] & 0xFFFFu;
               T x;
               if constexpr (ZZ)
                 x = (T)zz_dec((uint16_t)cd);
               else if constexpr (RK) {
                 const uint32_t zm = 0u - (uint32_t)(cd == 0u);  // all ones for a zero code
-                const uint32_t val = cv[rk];  // ranks past the prefetch: fixed below (reads stay in LDS)
-                const float cf = (float)cd;     // exact (codes < 2^16)
-                const uint32_t b = (val & zm) | (__builtin_bit_cast(uint32_t, cf) & ~zm);
+                const float cf = (float)cd;                      // exact (codes < 2^16)
+                const uint32_t b = (val[e] & zm) | (__builtin_bit_cast(uint32_t, cf) & ~zm);
                 x = (T)__builtin_bit_cast(float, b) - r;
                 rk -= zm;  // + 1 for a zero code
               }
@@ -1308,12 +1353,17 @@ k_brick1_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
                 x = (T)cd - r;
               v[2 * q + h] = x;
             }
+          }
         };
         if (ranked)
           values(std::true_type{});
         else
           values(std::false_type{});
+#ifndef CUSZ_AMD_EXP_NOFAR
         if (ranked && __builtin_amdgcn_ballot_w64(rk > npf)) {  // ranks past the prefetch (rare)
+#else
+        if (false) {
+#endif
           uint32_t j = 0;
 #pragma unroll
           for (int q = 0; q < 32; q++) {
@@ -1328,6 +1378,7 @@ k_brick1_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
           }
         }
         if (ranked) cur += rk;
+        BPROF(const unsigned long long tv = __builtin_readcyclecounter(); pc[8] += tv - tk;)
         if (!ranked) {  // values scattered into `out`: plane + zz_dec(0), or (plane + 0) - r
 #pragma unroll
           for (int q = 0; q < 32; q++) {
@@ -1346,56 +1397,125 @@ k_brick1_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
             }
           }
         }
-        // per thread: 4 sequential elements (wave32.cuhip.inl:10)
-#pragma unroll
-        for (int t = 0; t < 16; t++) {
-          v[4 * t + 1] = v[4 * t + 1] + v[4 * t];
-          v[4 * t + 2] = v[4 * t + 2] + v[4 * t + 1];
-          v[4 * t + 3] = v[4 * t + 3] + v[4 * t + 2];
-        }
-        // thread totals: Hillis-Steele over the segment's 32 (wave32.cuhip.inl:14-17), descending
-        // in place (each stage reads the previous stage's values); a[t] then holds thread t's
-        // inclusive total and thread t adds a[t - 1]
-        T a[32];
-        const int t0 = (blk & 1) ? 16 : 0;  // this block's threads are t0 .. t0 + 15
-#pragma unroll
-        for (int t = 0; t < 16; t++) {
-          if (blk & 1) a[t] = fh[t];
-          a[t0 + t] = v[4 * t + 3];
-          if (!(blk & 1)) fh[t] = v[4 * t + 3];
-        }
-        const int nt = t0 + 16;
-#pragma unroll
-        for (int d = 1; d < 32; d *= 2)
-#pragma unroll
-          for (int t = 31; t >= d; t--)
-            if (t < nt) a[t] = a[t] + a[t - d];
-        // add the previous thread's total, the segment carry, the scale; store the row piece
+        // per thread: 4 sequential elements (wave32.cuhip.inl:10); then the thread totals'
+        // Hillis-Steele over the segment's 32 (wave32.cuhip.inl:14-17), descending in place (each
+        // stage reads the previous stage's values): a[t] holds thread t's inclusive total and
+        // thread t adds a[t - 1]; then the segment carry and the scale.  f32: the same IEEE
+        // operations two at a time where the operands pair up (v_pk_add_f32 / v_pk_mul_f32).
         T tot = T(0);
+        auto scan = [&](auto otag) {
+          constexpr bool ODD = decltype(otag)::value;
+          constexpr int t0 = ODD ? 16 : 0, nt = t0 + 16;  // this block's threads: t0 .. t0 + 15
+          T a[32];
+          if constexpr (sizeof(T) == 4) {
+            typedef float f2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-        for (int t = 0; t < 16; t++) {
-          T o[4];
+            for (int k = 1; k < 4; k++)
 #pragma unroll
-          for (int k = 0; k < 4; k++) {
-            const T pv = (t0 + t > 0) ? v[4 * t + k] + a[t0 + t - 1] : v[4 * t + k];
-            o[k] = (pv + carry) * ebx2;
-            if (k == 3 && t == 15) tot = pv;  // the segment's total (second half)
+              for (int t = 0; t < 16; t += 2) {
+                f2 x = {v[4 * t + k], v[4 * t + 4 + k]};
+                x = x + f2{v[4 * t + k - 1], v[4 * t + 3 + k]};
+                v[4 * t + k] = x.x, v[4 * t + 4 + k] = x.y;
+              }
+#pragma unroll
+            for (int t = 0; t < 16; t++) {
+              if constexpr (ODD) a[t] = fh[t];
+              a[t0 + t] = v[4 * t + 3];
+              if constexpr (!ODD) fh[t] = v[4 * t + 3];
+            }
+#pragma unroll
+            for (int d = 1; d < 32; d *= 2) {
+              if (d >= nt) break;
+#pragma unroll
+              for (int t = nt - 1; t >= d; t -= 2) {
+                if (t - 1 >= d) {  // pair (t, t - 1): both sources still hold the previous stage
+                  f2 x = {a[t], a[t - 1]};
+                  x = x + f2{a[t - d], a[t - 1 - d]};
+                  a[t] = x.x, a[t - 1] = x.y;
+                }
+                else
+                  a[t] = a[t] + a[t - d];
+              }
+            }
           }
-          const uint32_t off = roff + (uint32_t)(4 * t) * (uint32_t)sizeof(T);
-          if (full)
-            buf_store4<T>(o, ro, off);
-          else
+          else {
 #pragma unroll
-            for (int k = 0; k < 4; k++) buf_store<T>(o[k], ro, off + (uint32_t)k * (uint32_t)sizeof(T), 0);
-        }
+            for (int t = 0; t < 16; t++) {
+              v[4 * t + 1] = v[4 * t + 1] + v[4 * t];
+              v[4 * t + 2] = v[4 * t + 2] + v[4 * t + 1];
+              v[4 * t + 3] = v[4 * t + 3] + v[4 * t + 2];
+            }
+#pragma unroll
+            for (int t = 0; t < 16; t++) {
+              if constexpr (ODD) a[t] = fh[t];
+              a[t0 + t] = v[4 * t + 3];
+              if constexpr (!ODD) fh[t] = v[4 * t + 3];
+            }
+#pragma unroll
+            for (int d = 1; d < 32; d *= 2)
+#pragma unroll
+              for (int t = nt - 1; t >= d; t--) a[t] = a[t] + a[t - d];
+          }
+#pragma unroll
+          for (int t = 0; t < 16; t++) {
+            T o[4];
+            if (t0 + t > 0) {
+#pragma unroll
+              for (int k = 0; k < 4; k++) v[4 * t + k] = v[4 * t + k] + a[t0 + t - 1];
+            }
+            if constexpr (sizeof(T) == 4) {
+              typedef float f2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+              for (int k = 0; k < 4; k += 2) {
+                f2 x = {v[4 * t + k], v[4 * t + k + 1]};
+                x = (x + f2{carry, carry}) * f2{ebx2, ebx2};
+                o[k] = x.x, o[k + 1] = x.y;
+              }
+            }
+            else {
+#pragma unroll
+              for (int k = 0; k < 4; k++) o[k] = (v[4 * t + k] + carry) * ebx2;
+            }
+            if (full) {
+              // through the tile's space (the codes are in registers): RE elements of every row
+              // per round (128 B), then each store instruction writes whole 128-B pieces of
+              // 64 / (RE / 4) rows instead of 16-B pieces of 64 rows
+              T* st = reinterpret_cast<T*>(tile);
+              constexpr uint32_t RE = 128 / sizeof(T), RT = RE / 4, LPR = RE / 4;  // elements, threads, lanes per row
+              constexpr uint32_t SP = RE + 16 / sizeof(T);  // row pitch (elements): 144 B
+              lds_store4<T>(st + lane * SP + 4u * (t % RT), o);
+              if (t % RT == RT - 1) {
+#pragma unroll
+                for (int m = 0; m < (int)(64 / (64 / LPR)); m++) {
+                  const uint32_t row = (64u / LPR) * m + (uint32_t)lane / LPR, sub = (uint32_t)lane % LPR;
+                  T w[4];
+                  lds_load4<T>(st + row * SP + 4u * sub, w);
+                  buf_store4<T>(w, ro, (row * 1024u + p * 256u + (uint32_t)blk * kBlk + RE * (t / RT) + 4u * sub) *
+                                           (uint32_t)sizeof(T));
+                }
+              }
+            }
+            else {
+              const uint32_t off = roff + (uint32_t)(4 * t) * (uint32_t)sizeof(T);
+#pragma unroll
+              for (int k = 0; k < 4; k++) buf_store<T>(o[k], ro, off + (uint32_t)k * (uint32_t)sizeof(T), 0);
+            }
+          }
+          if constexpr (ODD) tot = v[63];  // the segment's total
+        };
+        if (blk & 1)
+          scan(std::true_type{});
+        else
+          scan(std::false_type{});
         if (blk & 1) carry = carry + tot;
+        BPROF(pc[9] += __builtin_readcyclecounter() - tv;)
       };
       decode_chunks(tb, rg, dw, live, vbase, nbit, vlen, pro, blk_start, recon BPROF_A);
     }
   }
 #ifdef CUSZ_AMD_DEC_PROFILE
   if (lane == 0)
-    for (int i = 0; i < 8; i++) atomicAdd(&g_brick_prof[i], pc[i]);
+    for (int i = 0; i < 16; i++) atomicAdd(&g_brick_prof[i], pc[i]);
 #endif
 }
 
