@@ -199,6 +199,27 @@ __device__ __forceinline__ void store_brick_row(const BrickCodes& bcs, uint16_t*
   }
 }
 
+// The workgroup that finishes last copies pub.r to the host and raises pub.flag.  The ticket is a
+// relaxed atomic taken after the workgroup's barrier (which waits for its memory operations,
+// atomics included): the last workgroup reads the words back by agent-scope atomic loads.  (An
+// agent-scope release per workgroup would write back the XCD's L2 each time.)
+__device__ __forceinline__ void publish_last(const HostPub& pub)
+{
+  if (!pub.flag) return;
+  __shared__ uint32_t s_last;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(pub.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  for (int k = 0; k < pub.r.count; k++)
+    for (int i = threadIdx.x; i < pub.r.nwords[k]; i += blockDim.x)
+      pub.r.dst[k][i] = __hip_atomic_load(pub.r.src[k] + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(pub.flag, pub.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // End of a pass-1 unit: outlier count, row mask, the unit's histogram as a u16 record (16-B
 // stores, 8 bins per lane; the wave's LDS copy is cleared) and into the workgroup histogram.
 __device__ __forceinline__ void finish_unit(const OutlierSink& ol, const BrickCodes& bcs, uint32_t u, uint32_t cnt,
@@ -247,7 +268,7 @@ template <typename T, int V, bool ZZ>
 __global__ void __launch_bounds__(64 * kBrickWaves)
 k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T ebx2_r, T r, OutlierSink ol,
               uint32_t* __restrict__ g_hist, uint16_t* __restrict__ bhist, BrickCodes bcs, int bklen,
-              uint32_t nbx, uint32_t nby, uint32_t nbricks)
+              uint32_t nbx, uint32_t nby, uint32_t nbricks, HostPub pub)
 {
   extern __shared__ uint32_t smem[];
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wid: uniform (SGPR)
@@ -345,6 +366,7 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
     const uint32_t c = s_wg[i];
     if (c) atomicAdd(&g_hist[i], c);
   }
+  publish_last(pub);
 }
 
 // 1-D pass 1 (lrz_c.cuhip.inl:23-109): a brick is 64 consecutive chunks of W = 256 (16 tiles
@@ -356,7 +378,7 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
 template <typename T, int V, bool ZZ>
 __global__ void __launch_bounds__(64 * kBrickWaves)
 k_brick1_scan(const T* __restrict__ in, size_t n, T ebx2_r, T r, OutlierSink ol, uint32_t* __restrict__ g_hist,
-              uint16_t* __restrict__ bhist, BrickCodes bcs, int bklen, uint32_t nbricks)
+              uint16_t* __restrict__ bhist, BrickCodes bcs, int bklen, uint32_t nbricks, HostPub pub)
 {
   static_assert(V == 4, "W = 256");
   extern __shared__ uint32_t smem[];
@@ -442,6 +464,7 @@ k_brick1_scan(const T* __restrict__ in, size_t n, T ebx2_r, T r, OutlierSink ol,
     const uint32_t c = s_wg[i];
     if (c) atomicAdd(&g_hist[i], c);
   }
+  publish_last(pub);
 }
 
 // =========================================================================================
@@ -574,7 +597,7 @@ __global__ void __launch_bounds__(64 * kBrickWaves)
 k_brick3_pack(BrickCodes bcs, uint32_t ly, uint32_t lz, const uint32_t* __restrict__ book,
               int bklen, BrickPlanArgs pl, uint32_t* __restrict__ par_nbit, uint32_t* __restrict__ par_entry,
               uint32_t* __restrict__ bitstream, uint32_t nbx, uint32_t nby, uint32_t nbricks, int reverse,
-              unsigned int* overflow)
+              unsigned int* overflow, HostPub pub)
 {
   static_assert(V == 4, "8-B code loads");
   constexpr int CW = pack_cells_words<V>();
@@ -689,6 +712,8 @@ k_brick3_pack(BrickCodes bcs, uint32_t ly, uint32_t lz, const uint32_t* __restri
     if (off > lim && lane == 0) atomicOr(overflow, 1u);  // cannot happen (region is an upper bound)
     for (uint32_t i = off + lane; i < lim; i += 64) dst[i] = 0u;
   }
+  // the workgroup that finishes last publishes the compress summary (header, totals, status)
+  publish_last(pub);
 }
 
 // =========================================================================================
@@ -1582,7 +1607,8 @@ int brick_configure(BrickLaunch& L, int elem_bytes, int device)
 
 template <typename T>
 int launch_brick_scan(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const OutlierSink& ol,
-                      uint32_t* hist, uint16_t* bhist, const BrickCodes& bcodes, int bklen, hipStream_t st)
+                      uint32_t* hist, uint16_t* bhist, const BrickCodes& bcodes, int bklen, hipStream_t st,
+                      const HostPub& pub)
 {
   const T ebx2_r = (T)(1.0 / (eb * 2));  // lrz_c.cuhip.inl:489
   const T r = (T)radius;
@@ -1592,18 +1618,18 @@ int launch_brick_scan(const BrickLaunch& L, const T* in, double eb, int radius, 
   if (g.ndim == 1) {
     if (zz)
       k_brick1_scan<T, 4, true><<<grid, 64 * kBrickWaves, lds, st>>>(in, g.n, ebx2_r, r, ol, hist, bhist, bcodes, bklen,
-                                                                     g.nbricks);
+                                                                     g.nbricks, pub);
     else
       k_brick1_scan<T, 4, false><<<grid, 64 * kBrickWaves, lds, st>>>(in, g.n, ebx2_r, r, ol, hist, bhist, bcodes,
-                                                                      bklen, g.nbricks);
+                                                                      bklen, g.nbricks, pub);
     return (int)hipGetLastError();
   }
   if (zz)
     k_brick3_scan<T, 4, true><<<grid, 64 * kBrickWaves, lds, st>>>(in, L.lx, L.ly, L.lz, ebx2_r, r, ol, hist, bhist,
-                                                                   bcodes, bklen, g.nbx, g.nby, g.nbricks);
+                                                                   bcodes, bklen, g.nbx, g.nby, g.nbricks, pub);
   else
     k_brick3_scan<T, 4, false><<<grid, 64 * kBrickWaves, lds, st>>>(in, L.lx, L.ly, L.lz, ebx2_r, r, ol, hist, bhist,
-                                                                    bcodes, bklen, g.nbx, g.nby, g.nbricks);
+                                                                    bcodes, bklen, g.nbx, g.nby, g.nbricks, pub);
   return (int)hipGetLastError();
 }
 
@@ -1623,18 +1649,18 @@ int brick_hist_stride(int bklen) { return bhist_stride(bklen); }
 
 int launch_brick_pack(const BrickLaunch& L, const BrickCodes& bcodes, const uint32_t* book, int bklen,
                       const BrickPlanArgs& plan, uint32_t* par_nbit, uint32_t* par_entry, uint32_t* bitstream,
-                      int reverse, unsigned int* overflow, hipStream_t st)
+                      int reverse, unsigned int* overflow, hipStream_t st, const HostPub& pub)
 {
   const BrickGeom& g = L.g;
   const size_t lds = ((size_t)kMaxBklen + (size_t)kBrickWaves * pack_cells_words<4>()) * 4;
   if (g.ndim == 1)
     k_brick3_pack<4, 1><<<L.grid_pack, 64 * kBrickWaves, lds, st>>>(bcodes, L.ly, L.lz, book, bklen, plan, par_nbit,
                                                                     par_entry, bitstream, g.nbx, g.nby, g.nbricks,
-                                                                    reverse, overflow);
+                                                                    reverse, overflow, pub);
   else
     k_brick3_pack<4, 3><<<L.grid_pack, 64 * kBrickWaves, lds, st>>>(bcodes, L.ly, L.lz, book, bklen, plan, par_nbit,
                                                                     par_entry, bitstream, g.nbx, g.nby, g.nbricks,
-                                                                    reverse, overflow);
+                                                                    reverse, overflow, pub);
   return (int)hipGetLastError();
 }
 
@@ -1714,7 +1740,7 @@ extern "C" int psz_amd_debug_brick_profile(unsigned long long* host, int reset)
 
 #define INST(T)                                                                                                   \
   template int launch_brick_scan<T>(const BrickLaunch&, const T*, double, int, bool, const OutlierSink&, uint32_t*, \
-                                    uint16_t*, const BrickCodes&, int, hipStream_t);                               \
+                                    uint16_t*, const BrickCodes&, int, hipStream_t, const HostPub&);               \
   template int launch_brick_decode<T>(const BrickLaunch&, const uint32_t*, size_t, const uint8_t*, int,            \
                                       const uint32_t*, const uint32_t*, T*, double, int, bool, const BrickOutliers&, \
                                       hipStream_t);

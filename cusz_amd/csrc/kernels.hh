@@ -133,6 +133,9 @@ struct XferRegions {
 };
 int launch_publish(const XferRegions& r, uint32_t* flag, uint32_t epoch, hipStream_t st);
 int launch_upload(const XferRegions& r, hipStream_t st);
+// upload behind a device-polled host gate (the host sets *gate = epoch when the data is ready)
+int launch_gate_upload(const XferRegions& r, const uint32_t* gate, uint32_t epoch, unsigned int* timeout,
+                       hipStream_t st);
 int launch_zero(const XferRegions& r, hipStream_t st);  // dst/nwords only
 
 // ---- cuSZ-i spline3 (spline.hip) -----------------------------------------------------------
@@ -217,10 +220,19 @@ struct BrickCodes {
   uint64_t* rowmask;  // nbricks
   uint32_t c0;
 };
+// Words the last workgroup of a kernel copies to the host before raising a host flag (the
+// kernel's own publish: no separate launch).  ticket: a word zeroed before the launch.
+struct HostPub {
+  XferRegions r{};
+  uint32_t* flag = nullptr;  // null: no publish
+  uint32_t epoch = 0;
+  uint32_t* ticket = nullptr;
+};
 // pass 1: predict -> global + per-brick histograms, outliers, codes in brick order
 template <typename T>
 int launch_brick_scan(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const OutlierSink& ol,
-                      uint32_t* hist, uint16_t* bhist, const BrickCodes& bc, int bklen, hipStream_t st);
+                      uint32_t* hist, uint16_t* bhist, const BrickCodes& bc, int bklen, hipStream_t st,
+                      const HostPub& pub = HostPub{});
 // archive plan (brick.hip k_brick_plan): region sizes, cell / outlier offsets, totals, headers
 struct BrickPlanArgs {
   const uint16_t* bhist;  // per-brick histograms, stride brick_hist_stride(bklen)
@@ -254,7 +266,7 @@ int launch_brick_plan(const BrickLaunch& L, const BrickPlanArgs& a, const void* 
 // pass 2: brick-ordered codes -> Huffman cells at each brick's reserved region
 int launch_brick_pack(const BrickLaunch& L, const BrickCodes& bc, const uint32_t* book, int bklen,
                       const BrickPlanArgs& plan, uint32_t* par_nbit, uint32_t* par_entry, uint32_t* bitstream,
-                      int reverse, unsigned int* overflow, hipStream_t st);
+                      int reverse, unsigned int* overflow, hipStream_t st, const HostPub& pub = HostPub{});
 // Outlier cells for the fused decoder: when the archive's cells are grouped by brick and sorted
 // by (row, x) (k_brick_cell_bounds checks; this compressor writes them so), the decoder ranks the
 // zero codes of each row against the brick's cells and no scatter pass is needed; otherwise

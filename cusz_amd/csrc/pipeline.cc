@@ -123,8 +123,9 @@ struct Pipeline {
   // pinned, host-mapped, coherent transfer area (kernels write it, the host polls flags)
   uint8_t* h_xfer = nullptr;
   uint32_t epoch = 0;
-  uint32_t gate_epoch = 0;       // host -> stream gate (flag 5): the stream waits on it
-  bool can_wait_value = false;   // hipStreamWaitValue32 on host-mapped memory
+  uint32_t gate_epoch = 0;       // host -> stream gate (flag 5): the upload kernel polls it
+  uint32_t summary_epoch = 0;    // != 0: the compress summary is published by the pack kernel
+  bool gate = true;              // brick encode queued behind a device-polled host gate (flag 5)
   static constexpr size_t kXferBytes = 16384;
   volatile uint32_t* flag(int i) { return reinterpret_cast<volatile uint32_t*>(h_xfer) + i; }  // 0..15
   uint32_t* h_hist() { return reinterpret_cast<uint32_t*>(h_xfer + 64); }               // 4 KB
@@ -245,9 +246,7 @@ struct Pipeline {
     CUSZ_AMD_HIP_CHECK(hipHostMalloc(&h_xfer, kXferBytes, hipHostMallocMapped | hipHostMallocCoherent));
     std::memset(h_xfer, 0, kXferBytes);
     for (auto& e : ev) CUSZ_AMD_HIP_CHECK(hipEventCreate(&e));
-    int wv = 0;
-    if (hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, device) == hipSuccess) can_wait_value = wv;
-    if (const char* g = getenv("CUSZ_AMD_NO_GATE")) can_wait_value = can_wait_value && atoi(g) == 0;
+    if (const char* g = getenv("CUSZ_AMD_NO_GATE")) gate = atoi(g) == 0;
     return PSZ_SUCCESS;
   }
 
@@ -316,20 +315,23 @@ struct Pipeline {
   struct Pending {
     bool active = false, brick = false, spl = false, zz = false;
     int radius = 0;
+    uint32_t hist_epoch = 0;  // != 0: the scan published d_hist to h_hist() with this epoch (flag 2)
     size_t anchor_bytes = 0;
   } pend;
 
   template <typename T>
   int compress(psz_header* h, const T* in, uint8_t** out, size_t* outlen)
   {
-    const int s = compress_scan<T>(h, in);
+    const int s = compress_scan<T>(h, in, true);
     return s ? s : compress_finish(h, nullptr, out, outlen);
   }
 
   // Pass 1: [extrema] -> predict + histogram + outliers (+ codes).  The histogram stays on the
   // device (d_hist) for compress_finish, or for a caller that reduces it across slabs first.
+  // pub_hist: the brick scan publishes the histogram to the host itself (its last workgroup), for a
+  // finish that follows with the scan's own histogram
   template <typename T>
-  int compress_scan(psz_header* h, const T* in)
+  int compress_scan(psz_header* h, const T* in, bool pub_hist = false)
   {
     pend.active = false;
     const psz_predictor pred = h->pipeline.predictor;
@@ -386,8 +388,13 @@ struct Pipeline {
     pend.anchor_bytes = spl ? sizeof(T) * sgeom.anchor_len : 0;
     if (brick) {
       OutlierSink bol{d_slots, d_brick_cnt, d_spill, spill_cnt(), brick_cap(), spill_cap, nullptr};
+      HostPub hp;
+      if (pub_hist)
+        hp = HostPub{regions({{h_hist(), d_hist, (size_t)bklen * 4}}), const_cast<uint32_t*>(flag(2)), ++epoch,
+                     reinterpret_cast<uint32_t*>(d_small + 24)};
+      pend.hist_epoch = hp.epoch;
       CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_scan<T>(bl, in, eb, radius, zz, bol, d_hist, d_bhist,
-                                                          brick_codes(zz, radius), bklen, stream));
+                                                          brick_codes(zz, radius), bklen, stream, hp));
       mark(2);
       pend.active = true;
       return PSZ_SUCCESS;
@@ -435,7 +442,10 @@ struct Pipeline {
     if (!pend.active) return PSZ_ABORT_NOT_IMPLEMENTED;
     pend.active = false;
     const int radius = pend.radius, bklen = 2 * radius;
-    if (ext_hist) CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(d_hist, ext_hist, (size_t)bklen * 4, hipMemcpyDeviceToDevice, stream));
+    if (ext_hist) {
+      CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(d_hist, ext_hist, (size_t)bklen * 4, hipMemcpyDeviceToDevice, stream));
+      pend.hist_epoch = 0;  // the scan's published histogram is not the one to encode with
+    }
     if (pend.brick) return compress_brick(h, out, outlen, radius);
     const bool spl = pend.spl;
     const size_t anchor_bytes = pend.anchor_bytes;
@@ -509,16 +519,18 @@ struct Pipeline {
     const BrickGeom& g = bl.g;
     const int bsub = g.W, bpar = (int)g.nchunks;
     const uint32_t cap = brick_cap();
-    // The histogram goes to the host; the codebook comes back through host-mapped memory.  When
-    // the device supports stream waits, every launch after the codebook is queued NOW behind a
-    // gate the host opens once the book is built: the kernels start the moment it is ready
-    // instead of after their launch latency.
-    const uint32_t eh = ++epoch;
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_publish(regions({{h_hist(), d_hist, (size_t)bklen * 4}}),
-                                                  const_cast<uint32_t*>(flag(2)), eh, stream));
+    // The histogram goes to the host; the codebook comes back through host-mapped memory.  Every
+    // launch after the codebook is queued NOW: the upload kernel polls a host-mapped gate word the
+    // host sets once the book is built, so the encode kernels start right after it instead of
+    // after the host's launch latency (and without the command processor's stream-wait latency).
+    uint32_t eh = pend.hist_epoch;  // published by the scan's last workgroup, or now
+    if (!eh) {
+      eh = ++epoch;
+      CUSZ_AMD_HIP_CHECK((hipError_t)launch_publish(regions({{h_hist(), d_hist, (size_t)bklen * 4}}),
+                                                    const_cast<uint32_t*>(flag(2)), eh, stream));
+    }
     const uint32_t eg = ++gate_epoch;
-    const bool gated =
-        can_wait_value && hipStreamWaitValue32(stream, (void*)flag(5), eg, hipStreamWaitValueGte) == hipSuccess;
+    const bool gated = gate;
     // the gate must open on every path out of here, or the stream (and every later call on
     // it) waits forever: an early error return before build_book() opens it in the destructor
     struct GateGuard {
@@ -543,8 +555,14 @@ struct Pipeline {
     const size_t rvbk = rvbk_bytes(bklen);
     const size_t nbit_rel = 128 + rvbk, entry_rel = nbit_rel + 4 * (size_t)bpar;
     const size_t bits_rel = entry_rel + 4 * (size_t)bpar;
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_upload(
-        regions({{d_book, h_book(), (size_t)bklen * 4}, {d_archive + phf_off + 128, h_revbook(), rvbk}}), stream));
+    {
+      const XferRegions up =
+          regions({{d_book, h_book(), (size_t)bklen * 4}, {d_archive + phf_off + 128, h_revbook(), rvbk}});
+      if (gated)
+        CUSZ_AMD_HIP_CHECK((hipError_t)launch_gate_upload(up, const_cast<const uint32_t*>(flag(5)), eg, timeout(), stream));
+      else
+        CUSZ_AMD_HIP_CHECK((hipError_t)launch_upload(up, stream));
+    }
     mark(3);
 
     uint32_t* par_nbit = reinterpret_cast<uint32_t*>(d_archive + phf_off + nbit_rel);
@@ -568,8 +586,11 @@ struct Pipeline {
                      d_plan, d_plan + nblk + 1, info(), d_archive, phf_off, bits_rel};
     pa.nd = (uint32_t)g.ndim, pa.nchunks = g.nchunks, pa.n = g.n;
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_plan(bl, pa, h, &ph, stream));
+    // the pack's last workgroup publishes the summary finish_compress reads (no publish launch)
+    const HostPub sp{readback_regions(), const_cast<uint32_t*>(flag(3)), ++epoch, reinterpret_cast<uint32_t*>(d_small + 20)};
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_pack(bl, brick_codes(pend.zz, radius), d_book, bklen, pa, par_nbit, par_entry, bits,
-                                                     pack_reverse, timeout(), stream));
+                                                     pack_reverse, timeout(), stream, sp));
+    summary_epoch = sp.epoch;
     mark(4);
     if (gated)
       if (int fs = build_book()) return fs;
@@ -578,12 +599,18 @@ struct Pipeline {
   }
 
   // read back the device-written header + summary (one flag wait), report status
+  XferRegions readback_regions()
+  {
+    return regions({{h_readback(), d_archive, 176},
+                    {h_readback() + 256, info(), sizeof(CompressInfo)},
+                    {h_readback() + 384, timeout(), 4}});
+  }
+
   int finish_compress(psz_header* h, uint8_t** out, size_t* outlen)
   {
-    int fs = fetch(regions({{h_readback(), d_archive, 176},
-                            {h_readback() + 256, info(), sizeof(CompressInfo)},
-                            {h_readback() + 384, timeout(), 4}}),
-                   3);
+    const uint32_t se = summary_epoch;
+    summary_epoch = 0;
+    int fs = se ? wait_flag(3, se) : fetch(readback_regions(), 3);
     if (fs) return fs;
     if (timing) CUSZ_AMD_HIP_CHECK(hipEventSynchronize(ev[5]));
     CompressInfo ci;

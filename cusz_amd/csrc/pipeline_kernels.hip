@@ -257,7 +257,46 @@ __global__ void __launch_bounds__(256) k_upload(XferRegions r)
     for (int i = blockIdx.x * 256 + threadIdx.x; i < r.nwords[k]; i += gridDim.x * 256) r.dst[k][i] = r.src[k][i];
 }
 
+// Copy host-mapped words into device memory once the host has opened the gate (*gate reaches
+// epoch: the codebook is built).  One thread per workgroup polls the host word with system-scope
+// acquire loads; then every thread copies at most a word or two (each read crosses PCIe, so the
+// copy is spread over kGateBlocks workgroups).  A poller gives up after a few seconds and flags
+// the timeout word (the host always opens the gate, also on its error paths).
+__global__ void __launch_bounds__(256) k_gate_upload(XferRegions r, const uint32_t* gate, uint32_t epoch,
+                                                     unsigned int* timeout)
+{
+  __shared__ uint32_t s_ok;
+  if (threadIdx.x == 0) {
+    uint32_t ok = 1;
+    for (uint32_t spin = 0;; spin++) {
+      const uint32_t v = __hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if ((int32_t)(v - epoch) >= 0) break;
+      if (spin > (1u << 22)) {
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    s_ok = ok;
+  }
+  __syncthreads();
+  if (!s_ok) {
+    if (threadIdx.x == 0) atomicOr(timeout, 2u);
+    return;
+  }
+  for (int k = 0; k < r.count; k++)
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < r.nwords[k]; i += gridDim.x * 256) r.dst[k][i] = r.src[k][i];
+}
+
 }  // namespace
+
+int launch_gate_upload(const XferRegions& r, const uint32_t* gate, uint32_t epoch, unsigned int* timeout,
+                       hipStream_t st)
+{
+  constexpr int kGateBlocks = 8;
+  k_gate_upload<<<kGateBlocks, 256, 0, st>>>(r, gate, epoch, timeout);
+  return (int)hipGetLastError();
+}
 
 int launch_publish(const XferRegions& r, uint32_t* flag, uint32_t epoch, hipStream_t st)
 {
