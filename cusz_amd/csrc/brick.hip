@@ -375,10 +375,14 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
 // 63 of the previous row, 0 at a tile start.  Rows are loaded kScanAhead ahead (register queue,
 // raw buffer loads from the brick's origin, past the field's end they read 0); codes, histograms,
 // outlier slots and row masks as in the 3-D pass.
-template <typename T, int V, bool ZZ>
+//
+// 2-D fields use the same linear bricks (ND = 2, lx % 4 == 0, lx >= 256): the predictor is the
+// reference's 2-D one (lrz_c.cuhip.inl:187-273, 32 x 32 tiles: a = p - p(north) unless y % 32 == 0,
+// then d = a - a(west) unless x % 32 == 0), the north row coming from a second load queue.
+template <typename T, int V, bool ZZ, int ND>
 __global__ void __launch_bounds__(64 * kBrickWaves)
 k_brick1_scan(const T* __restrict__ in, size_t n, T ebx2_r, T r, OutlierSink ol, uint32_t* __restrict__ g_hist,
-              uint16_t* __restrict__ bhist, BrickCodes bcs, int bklen, uint32_t nbricks, HostPub pub)
+              uint16_t* __restrict__ bhist, BrickCodes bcs, int bklen, uint32_t nbricks, HostPub pub, uint32_t lx)
 {
   static_assert(V == 4, "W = 256");
   extern __shared__ uint32_t smem[];
@@ -406,10 +410,42 @@ k_brick1_scan(const T* __restrict__ in, size_t n, T ebx2_r, T r, OutlierSink ol,
       __builtin_memcpy(reinterpret_cast<char*>(&dst[0]) + 16 * h, &v, 16);
     }
   };
+  // 2-D: the north row (element i - lx) of the row issued, by a whole-field resource (the field is
+  // < 2^31 bytes, brick_geom); rows on a tile's first line (y % 32 == 0) read 0 past its range.
+  // (xi, yi) is the issue cursor of this lane's first element, (xl, yl) the compute cursor.
+  const __amdgpu_buffer_rsrc_t rsall =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(in), 0, (int)(ND == 2 ? n * sizeof(T) : 0), 0x00020000);
+  uint32_t xi = 0, yi = 0;
+  auto cursor_at = [&](uint32_t b, uint32_t& x, uint32_t& y) {
+    const size_t i = (size_t)b * kBE + x0;
+    x = (uint32_t)(i % lx), y = (uint32_t)(i / lx);
+  };
+  auto advance = [&](uint32_t& x, uint32_t& y) {  // next row: + 64 V elements (lx >= 64 V)
+    x += 64 * V;
+    if (x >= lx) x -= lx, y++;
+  };
+  auto issue_north = [&](uint32_t b, uint32_t x, uint32_t y, T (&dst)[V]) {
+    if (b >= nbricks) return;
+    const size_t i = (size_t)y * lx + x;
+    const uint32_t off = (y % 32u != 0u) ? (uint32_t)((i - lx) * sizeof(T)) : 0x80000000u;
+#pragma unroll
+    for (int h = 0; h < (int)(V * sizeof(T) / 16); h++) {
+      const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rsall, (int)(off + 16 * h), 0, 0);
+      __builtin_memcpy(reinterpret_cast<char*>(&dst[0]) + 16 * h, &v, 16);
+    }
+  };
   uint32_t u = blockIdx.x * kBrickWaves + wid;
   T q[D][V];
+  T qn[ND == 2 ? D : 1][V];
+  if constexpr (ND == 2) cursor_at(u, xi, yi);
 #pragma unroll
-  for (int j = 0; j < D; j++) issue_row(u, j, q[j]);
+  for (int j = 0; j < D; j++) {
+    issue_row(u, j, q[j]);
+    if constexpr (ND == 2) {
+      issue_north(u, xi, yi, qn[j]);
+      advance(xi, yi);
+    }
+  }
   for (; u < nbricks; u += nw) {
     uint32_t cnt = 0;
     uint64_t rowmask = 0;
@@ -417,7 +453,20 @@ k_brick1_scan(const T* __restrict__ in, size_t n, T ebx2_r, T r, OutlierSink ol,
     const bool full = n - bbase >= kBE;  // no element past the field's end (uniform)
     uint16_t* cbrick = bcs.c16 + bbase + x0;
     uint8_t* cbrick8 = bcs.c8 + bbase + x0;
-    T carry = 0;  // prequant of the previous row's last element
+    T carry = 0;  // 1-D: prequant, 2-D: y-difference, of the previous row's last element
+    uint32_t xl = 0, yl = 0;
+    if constexpr (ND == 2) {
+      cursor_at(u, xl, yl);
+      // a brick starts on a 1-D tile boundary, not on a 2-D one: the element before it belongs
+      // to the previous brick (a is needed when it lies in the same 32-wide tile row)
+      if (bbase > 0) {
+        const size_t i = bbase - 1;
+        const uint32_t y = (uint32_t)(i / lx);
+        T a = dround(in[i] * ebx2_r);
+        if (y % 32u != 0u) a = a - dround(in[i - lx] * ebx2_r);
+        carry = a;
+      }
+    }
 #pragma unroll 1
     for (int r0 = 0; r0 < 64; r0 += D)
 #pragma unroll
@@ -426,18 +475,33 @@ k_brick1_scan(const T* __restrict__ in, size_t n, T ebx2_r, T r, OutlierSink ol,
         T p[V];
 #pragma unroll
         for (int k = 0; k < V; k++) p[k] = dround(q[j][k] * ebx2_r);
+        if constexpr (ND == 2) {  // a = p - p(north): 0 past the field / on a tile's first line
+#pragma unroll
+          for (int k = 0; k < V; k++) p[k] = p[k] - dround(qn[j][k] * ebx2_r);
+        }
+        const uint32_t bnext = row + D < 64 ? u : u + nw;
         if (row + D < 64) issue_row(u, row + D, q[j]);
         else issue_row(u + nw, row + D - 64, q[j]);
+        if constexpr (ND == 2) {
+          if (row + D == 64) cursor_at(u + nw, xi, yi);  // the queue moves on to the next brick
+          issue_north(bnext, xi, yi, qn[j]);
+          advance(xi, yi);
+        }
         const size_t base = bbase + (size_t)row * (64 * V);
         T west = __shfl_up(p[V - 1], 1);
         const T last = __shfl(p[V - 1], 63);
-        if (lane == 0) west = (row & 3) ? carry : T(0);
+        if (lane == 0) west = (ND == 2 || (row & 3)) ? carry : T(0);
         carry = last;
+        const uint32_t xcur = xl;
+        if constexpr (ND == 2) advance(xl, yl);
         if (!full && base >= n) continue;  // past the field's end (uniform)
         T d[V];
 #pragma unroll
         for (int k = V - 1; k > 0; k--) d[k] = p[k] - p[k - 1];
-        d[0] = p[0] - west;
+        if constexpr (ND == 2)
+          d[0] = (xcur % 32u != 0u) ? p[0] - west : p[0];  // x % 32 == 0: a tile's first column
+        else
+          d[0] = p[0] - west;
         float olv[V];
         uint16_t qc[V];
         uint32_t mask = 0;
@@ -1557,8 +1621,9 @@ BrickGeom brick_geom(int ndim, size_t lx, size_t ly, size_t lz, int elem_bytes)
   g.W = 64 * g.V;
   g.ndim = ndim;
   g.n = lx * ly * lz;
-  if (ndim == 1) {
-    g.ok = g.n < (1ull << 32) && (elem_bytes == 4 || elem_bytes == 8);
+  if (ndim == 1 || ndim == 2) {  // linear bricks (2-D: x extent a multiple of 4, >= 256; < 2 GiB)
+    g.ok = g.n < (1ull << 32) && (elem_bytes == 4 || elem_bytes == 8) &&
+           (ndim == 1 || (lx % 4 == 0 && lx >= (size_t)g.W && g.n * elem_bytes < (1ull << 31)));
     if (!g.ok) return g;
     g.brick_elems = (uint32_t)g.W * 64;
     g.nbricks = (uint32_t)((g.n + g.brick_elems - 1) / g.brick_elems);
@@ -1615,13 +1680,17 @@ int launch_brick_scan(const BrickLaunch& L, const T* in, double eb, int radius, 
   const BrickGeom& g = L.g;
   const size_t lds = (size_t)(1 + kBrickWaves * kHistCopies) * kMaxBklen * 4;
   const int grid = L.grid_scan;
-  if (g.ndim == 1) {
-    if (zz)
-      k_brick1_scan<T, 4, true><<<grid, 64 * kBrickWaves, lds, st>>>(in, g.n, ebx2_r, r, ol, hist, bhist, bcodes, bklen,
-                                                                     g.nbricks, pub);
-    else
-      k_brick1_scan<T, 4, false><<<grid, 64 * kBrickWaves, lds, st>>>(in, g.n, ebx2_r, r, ol, hist, bhist, bcodes,
-                                                                      bklen, g.nbricks, pub);
+  if (g.ndim == 1 || g.ndim == 2) {
+#define SCAN1(ZZ, ND)                                                                                           \
+  k_brick1_scan<T, 4, ZZ, ND><<<grid, 64 * kBrickWaves, lds, st>>>(in, g.n, ebx2_r, r, ol, hist, bhist, bcodes, \
+                                                                   bklen, g.nbricks, pub, L.lx)
+    if (g.ndim == 1) {
+      if (zz) SCAN1(true, 1); else SCAN1(false, 1);
+    }
+    else {
+      if (zz) SCAN1(true, 2); else SCAN1(false, 2);
+    }
+#undef SCAN1
     return (int)hipGetLastError();
   }
   if (zz)
@@ -1653,7 +1722,7 @@ int launch_brick_pack(const BrickLaunch& L, const BrickCodes& bcodes, const uint
 {
   const BrickGeom& g = L.g;
   const size_t lds = ((size_t)kMaxBklen + (size_t)kBrickWaves * pack_cells_words<4>()) * 4;
-  if (g.ndim == 1)
+  if (g.ndim != 3)
     k_brick3_pack<4, 1><<<L.grid_pack, 64 * kBrickWaves, lds, st>>>(bcodes, L.ly, L.lz, book, bklen, plan, par_nbit,
                                                                     par_entry, bitstream, g.nbx, g.nby, g.nbricks,
                                                                     reverse, overflow, pub);

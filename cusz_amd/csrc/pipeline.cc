@@ -79,6 +79,7 @@ struct Pipeline {
   LorenzoGeom geom{};
   BrickLaunch bl{};               // fused brick path (brick.hip); bl.g.ok when eligible
   int layout = 0;                 // PSZ_AMD_LAYOUT_*: 0 brick layout when eligible, 1 reference layout
+  bool layout_set = false;        // the caller chose the layout (psz_amd_set_layout)
   uint16_t* d_bhist = nullptr;    // per-brick u16 histograms (pass 1 -> reservation)
   uint32_t* d_ub = nullptr;       // per-brick region upper bounds (cells)
   uint32_t* d_bbase = nullptr;    // per-brick cell offsets inside their plan block
@@ -179,7 +180,10 @@ struct Pipeline {
   // fused brick path: 3-D, eligible shape, Lorenzo, default chunking (chunk = brick row)
   bool use_brick(psz_predictor pred) const
   {
-    return bl.g.ok && layout == 0 && (pred == Lorenzo || pred == LorenzoZigZag) &&
+    // 2-D linear bricks by default only when there are enough to fill the device (a wave walks a
+    // brick serially: 3600 x 1800 has 396, the reference layout is faster there)
+    const bool enough = bl.g.ndim != 2 || layout_set || bl.g.nbricks >= 4u * (uint32_t)bl.ncu;
+    return bl.g.ok && layout == 0 && enough && (pred == Lorenzo || pred == LorenzoZigZag) &&
            (user_sublen == 0 || user_sublen == bl.g.W);
   }
 
@@ -584,7 +588,7 @@ struct Pipeline {
     BrickPlanArgs pa{d_bhist, bklen, brick_hist_stride(bklen), d_book, g.nbricks, brick_units(g.nbricks), g.nbx, g.nby, bl.ly, bl.lz,
                      d_brick_cnt, cap, d_slots, d_spill, spill_cnt(), spill_cap, nblk, d_ub, d_bbase, d_brick_off,
                      d_plan, d_plan + nblk + 1, info(), d_archive, phf_off, bits_rel};
-    pa.nd = (uint32_t)g.ndim, pa.nchunks = g.nchunks, pa.n = g.n;
+    pa.nd = g.ndim == 3 ? 3u : 1u, pa.nchunks = g.nchunks, pa.n = g.n;  // 1-D and 2-D: linear bricks
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_plan(bl, pa, h, &ph, stream));
     // the pack's last workgroup publishes the summary finish_compress reads (no publish launch)
     const HostPub sp{readback_regions(), const_cast<uint32_t*>(flag(3)), ++epoch, reinterpret_cast<uint32_t*>(d_small + 20)};
@@ -679,7 +683,9 @@ struct Pipeline {
     if (h->len.x != len.x || h->len.y != len.y || h->len.z != len.z) return PSZ_ABORT_UNSUPPORTED_DIMENSION;
     if (pred == Spline) return decompress_spline<T>(h, in, out);
     mark(6);
-    const bool brickdec = bl.g.ok && decoder == 0 && h->vle_sublen == bl.g.W && 2 * h->rc.radius <= kMaxBklen;
+    // fused decode + reconstruct: 3-D and 1-D (2-D linear-brick archives decode chunk by chunk)
+    const bool brickdec = bl.g.ok && bl.g.ndim != 2 && decoder == 0 && h->vle_sublen == bl.g.W &&
+                          2 * h->rc.radius <= kMaxBklen;
     const uint32_t* cells = reinterpret_cast<const uint32_t*>(in + h->entry[PSZHEADER_SPFMT]);
     X1dOutliers ox;  // 1-D: the reconstruction reads sorted cells directly (no scatter pass)
     if (geom.ndim == 1 && d_x1d && !zz && !brickdec && h->splen) {
@@ -1080,6 +1086,7 @@ int psz_amd_set_layout(psz_resource* m, int layout)
   Pipeline* p = cusz_amd::P(m);
   if (!p || (layout != PSZ_AMD_LAYOUT_BRICK && layout != PSZ_AMD_LAYOUT_REFERENCE)) return PSZ_ABORT_NOT_IMPLEMENTED;
   p->layout = layout;
+  p->layout_set = true;
   return PSZ_SUCCESS;
 }
 

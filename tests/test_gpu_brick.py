@@ -43,6 +43,12 @@ CASES = [
     ((50_000, 1, 1), np.float32, 1e-2, False, 512, "noise"),
     ((50_000, 1, 1), np.float32, 1e-3, False, 64, "hacc"),     # many outliers per block row
     ((40_000, 1, 1), np.float32, 0.5, False, 512, "int"),
+    # 2-D on linear bricks (x % 4 == 0, x >= 256): 2-D predictor, chunks in index order
+    ((3600, 90, 1), np.float32, 1e-4, False, 512, "cesm"),
+    ((300, 97, 1), np.float32, 1e-4, False, 512, "cesm"),
+    ((1024, 33, 1), np.float64, 1e-4, False, 512, "cesm"),
+    ((3600, 40, 1), np.float32, 1e-4, True, 512, "cesm"),
+    ((512, 64, 1), np.float32, 1e-2, False, 512, "noise"),
 ]
 
 
@@ -55,6 +61,8 @@ def _field(kind, dims, dtype, seed):
         return rng.standard_normal(n).astype(dtype)
     if kind == "hacc":
         return datagen.hacc1d_np(n, seed).astype(dtype)
+    if kind == "cesm":
+        return datagen.cesm2d_np(dims[:2], seed).astype(dtype).reshape(-1)
     return np.cumsum(rng.integers(-3, 4, n)).astype(dtype)
 
 
@@ -63,7 +71,9 @@ def _field(kind, dims, dtype, seed):
                               for c in CASES])
 def test_brick_parity(oracle, dims, dtype, eb, zz, radius, kind):
     data = _field(kind, dims, dtype, seed=sum(dims))
-    arch, a = run_roundtrip(oracle, data, dims, eb, dtype, zz, radius, check_bound=kind != "noise")
+    # 2-D fields this small take the reference layout by default (too few bricks): force bricks
+    layout = cz.LAYOUT_BRICK if dims[1] > 1 and dims[2] == 1 else None
+    arch, a = run_roundtrip(oracle, data, dims, eb, dtype, zz, radius, check_bound=kind != "noise", layout=layout)
     assert a["sublen"] == 256, "brick layout expected"
 
 

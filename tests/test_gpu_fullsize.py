@@ -75,6 +75,9 @@ def test_config1_cesm_2d(oracle):
     d_in = torch.from_numpy(host).cuda()
     r = cz.Resource(cz.F4, dims)
     ptr, nbytes, _ = r.compress(d_in.data_ptr(), 1e-4)
+    if r.internals().layout == cz.LAYOUT_BRICK:  # the codes never reach HBM in index order
+        r.decode_codes(ptr)
+        sync()
     c_o, ov, oi = oracle.lorenzo_c(host, dims, 1e-4)
     np.testing.assert_array_equal(d2h(r.internals().d_quant_codes, 2 * host.size, np.uint16), c_o)
     out = empty_device(host.size, torch.float32)
