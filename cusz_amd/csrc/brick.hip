@@ -177,8 +177,9 @@ __device__ __forceinline__ void store_codes_row(uint16_t* p, const uint16_t (&q)
   *reinterpret_cast<uint2*>(p) = w;
 }
 
-// One brick row of codes between the encode passes: bytes (code - c0) when every code of the
-// row fits [c0, c0 + 254], else u16 with the row's bit set in the brick's row mask (BrickCodes).
+// One brick row of codes between the encode passes: bytes (code - c0, and 255 for the outlier
+// code 0) when every code of the row fits [c0, c0 + 254] or is 0, else u16 with the row's bit set
+// in the brick's row mask (BrickCodes).  Code 0 is always stored as 255 (never code - c0).
 template <int V>
 __device__ __forceinline__ void store_brick_row(const BrickCodes& bcs, uint16_t* cbrick, uint8_t* cbrick8, int row,
                                                 const uint16_t (&qc)[V], uint64_t& rowmask)
@@ -186,7 +187,7 @@ __device__ __forceinline__ void store_brick_row(const BrickCodes& bcs, uint16_t*
   static_assert(V == 4, "one 4-B byte-code store per lane and row");
   bool wide = false;
 #pragma unroll
-  for (int k = 0; k < V; k++) wide |= (uint32_t)qc[k] - bcs.c0 > 254u;
+  for (int k = 0; k < V; k++) wide |= (uint32_t)qc[k] - bcs.c0 > 254u && qc[k] != 0;
   if (__builtin_amdgcn_ballot_w64(wide)) {
     store_codes_row<V>(cbrick + (size_t)row * (64 * V), qc);
     rowmask |= 1ull << row;
@@ -194,7 +195,7 @@ __device__ __forceinline__ void store_brick_row(const BrickCodes& bcs, uint16_t*
   else {
     uint32_t w = 0;
 #pragma unroll
-    for (int k = 0; k < V; k++) w |= ((uint32_t)qc[k] - bcs.c0) << (8 * k);
+    for (int k = 0; k < V; k++) w |= (qc[k] == 0 ? 255u : (uint32_t)qc[k] - bcs.c0) << (8 * k);
     *reinterpret_cast<uint32_t*>(cbrick8 + (size_t)row * (64 * V)) = w;
   }
 }
@@ -737,7 +738,10 @@ k_brick3_pack(BrickCodes bcs, uint32_t ly, uint32_t lz, const uint32_t* __restri
           }
           else {
 #pragma unroll
-            for (int k = 0; k < 4; k++) qs[k] = ((cur[z].x >> (8 * k)) & 255u) + bcs.c0;
+            for (int k = 0; k < 4; k++) {
+              const uint32_t b = (cur[z].x >> (8 * k)) & 255u;
+              qs[k] = b == 255u ? 0u : b + bcs.c0;  // 255: the outlier code 0
+            }
           }
           uint32_t w[V], bits = 0;
           // 1-D: the field's last chunk may be short; codes past its end get no codeword

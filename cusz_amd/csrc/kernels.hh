@@ -211,7 +211,8 @@ struct BrickLaunch {
 int brick_configure(BrickLaunch& L, int elem_bytes, int device);
 
 // Quant codes between the two encode passes, in brick order (row r of brick b at (64 b + r) W).
-// A row whose codes all lie in [c0, c0 + 254] is stored as bytes (code - c0) in c8; any other
+// A row whose codes all lie in [c0, c0 + 254] or are 0 (outliers) is stored as bytes (code - c0;
+// 255 for code 0) in c8; any other
 // row as u16 codes in c16, with bit r of rowmask[b] set.  c0 = radius - 127 (ZigZag: 0): the
 // rows that are not u16 are about 90 % of a smooth field's (those off the tiles' first z plane).
 struct BrickCodes {

@@ -100,6 +100,9 @@ def test_config3_hacc_1d_ragged(oracle):
     ptr, nbytes, _ = r.compress(d_in.data_ptr(), 1e-4)
     h = r.header
     ino = r.internals()
+    if ino.layout == cz.LAYOUT_BRICK:  # the codes never reach HBM in index order: decode them
+        r.decode_codes(ptr)
+        sync()
     # tail tile against the oracle (tile-independence), including the ragged last tile
     tail0 = (n // 1024 - 3) * 1024
     sub = d_in[tail0:].cpu().numpy()
