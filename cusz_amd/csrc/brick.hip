@@ -1121,17 +1121,16 @@ struct DecWave {
   int lane;
 };
 
-// Decode one chunk per lane (chunk bits at word vbase / 4, nbit bits, vlen <= 256 symbols; a dead
+// Decode one chunk per lane (chunk bits at word vbase / 4, nbit bits, vlen <= W symbols; a dead
 // lane decodes nothing) in W / kBlk blocks of kBlk columns into the tile; after each block the
 // wave calls recon(blk).  pro() runs while the first words are in flight; blk_start(blk) before
-// each block's decode.
+// each block's decode.  W: the chunk length (a multiple of kBlk; 256 in the fused decoders).
 template <class Pro, class BlkStart, class Recon>
 __device__ __forceinline__ void decode_chunks(const hfd::LdsTables<kDecB>& tb, const hfd::DecRegs& rg,
                                               const DecWave& dw, bool live, uint32_t vbase, uint32_t nbit,
                                               uint32_t vlen, Pro&& pro, BlkStart&& blk_start,
-                                              Recon&& recon BPROF_P)
+                                              Recon&& recon BPROF_P, uint32_t W = 256)
 {
-  constexpr uint32_t W = 256;
   const int lane = dw.lane;
   uint32_t* ring_lane = dw.ring_lane;
   const uint32_t nwords = (nbit + 31u) >> 5;
@@ -1612,6 +1611,55 @@ k_brick1_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
 #endif
 }
 
+// ---- decode only: any layout -> codes in index order ------------------------------------------
+// The fused decoders' chunk loop with the tile copied out instead of reconstructed: wave u
+// decodes chunks [64 u, 64 u + 64) (lane = chunk), and after each block of 64 columns stores the
+// tile as codes (two rows of 128 B per store instruction).  Used for every archive (chunk length
+// a multiple of 64) the fused decoders do not take: 2-D, spline, the reference layout, a
+// standalone decode of the codes.
+template <int DUMMY>
+__global__ void __launch_bounds__(64 * kDecWaves)
+k_chunk_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const uint8_t* __restrict__ revbook,
+               int bklen, const uint32_t* __restrict__ par_nbit, const uint32_t* __restrict__ par_entry,
+               uint16_t* __restrict__ codes, size_t n, uint32_t nchunks, uint32_t sublen)
+{
+  __shared__ hfd::LdsTables<kDecB> tb;
+  extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
+  hfd::build_tables<kDecB>(tb, revbook, bklen);
+  const hfd::DecRegs rg = hfd::load_dec_regs(tb);
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* wbase = dsm + (size_t)wid * kDecRows;  // ring + tile (no cell staging)
+  uint16_t* tile = reinterpret_cast<uint16_t*>(wbase + kDecTile);
+  const DecWave dw{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(bitstream), 0, (int)(bs_words * 4u), (int)kBufRsrcW3),
+                   reinterpret_cast<uint32_t*>(wbase) + lane, tile, (uint32_t)bklen, lane};
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  const uint32_t nunits = (nchunks + 63) / 64;
+  BPROF(unsigned long long pc[16] = {}; unsigned long long tk = __builtin_readcyclecounter(), tp = tk;)
+  for (uint32_t u = blockIdx.x * (blockDim.x >> 6) + wid; u < nunits; u += nw) {
+    const size_t c = (size_t)u * 64u + (uint32_t)lane;
+    const bool live = c < nchunks;
+    const uint32_t nbit = live ? par_nbit[c] : 0u;
+    const uint32_t vbase = (live ? par_entry[c] : 0u) * 4u;
+    const uint32_t vlen = live ? (uint32_t)min((size_t)sublen, n - c * sublen) : 0u;
+    auto recon = [&](int blk) {
+      const uint32_t* t32 = reinterpret_cast<const uint32_t*>(tile);
+      const uint32_t cp = (uint32_t)lane & 31u;  // column pair
+#pragma unroll 4
+      for (uint32_t it = 0; it < 32; it++) {
+        const uint32_t row = 2u * it + ((uint32_t)lane >> 5);
+        const uint32_t w = t32[row * (kTP / 2) + cp];
+        const size_t e = ((size_t)u * 64u + row) * sublen + (uint32_t)blk * kBlk + 2u * cp;
+        if ((uint32_t)blk * kBlk + 2u * cp >= sublen) continue;  // (sublen is a multiple of kBlk)
+        if (e + 1 < n)
+          *reinterpret_cast<uint32_t*>(codes + e) = w;
+        else if (e < n)
+          codes[e] = (uint16_t)w;
+      }
+    };
+    decode_chunks(tb, rg, dw, live, vbase, nbit, vlen, [] {}, [](int) {}, recon BPROF_A, sublen);
+  }
+}
+
 }  // namespace
 
 // =========================================================================================
@@ -1796,6 +1844,22 @@ int launch_brick_decode(const BrickLaunch& L, const uint32_t* bitstream, size_t 
     if (buf) DEC_LAUNCH(false, true); else DEC_LAUNCH(false, false);
   }
 #undef DEC_LAUNCH
+  return (int)hipGetLastError();
+}
+
+
+int launch_chunk_decode(const BrickLaunch& L, const uint32_t* bitstream, size_t bs_words, const uint8_t* revbook,
+                        int bklen, const uint32_t* par_nbit, const uint32_t* par_entry, uint16_t* codes, size_t n,
+                        uint32_t nchunks, uint32_t sublen, hipStream_t st)
+{
+  if (bs_words >= (1ull << 30) || bklen < 1 || bklen > kMaxBklen || sublen % kBlk != 0 || sublen == 0)
+    return (int)hipErrorInvalidValue;
+  if (!nchunks) return (int)hipSuccess;
+  const size_t lds = (size_t)kDecWaves * kDecRows;
+  const uint32_t units = (nchunks + 63) / 64;
+  const uint32_t grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(L.ncu > 0 ? L.ncu : 256, (units + kDecWaves - 1) / kDecWaves));
+  k_chunk_decode<0><<<grid, 64 * kDecWaves, lds, st>>>(bitstream, (uint32_t)bs_words, revbook, bklen, par_nbit,
+                                                       par_entry, codes, n, nchunks, sublen);
   return (int)hipGetLastError();
 }
 

@@ -281,6 +281,11 @@ struct BrickOutliers {
 };
 int launch_brick_cell_bounds(const BrickLaunch& L, const uint32_t* cells, size_t ncell, uint32_t* bstart,
                              uint32_t* unsorted, uint32_t epoch, hipStream_t st);
+// decode only, any archive whose chunk length is a multiple of 64: chunk c's codes to
+// codes[sublen c ...] (index order)
+int launch_chunk_decode(const BrickLaunch& L, const uint32_t* bitstream, size_t bs_words, const uint8_t* revbook,
+                        int bklen, const uint32_t* par_nbit, const uint32_t* par_entry, uint16_t* codes, size_t n,
+                        uint32_t nchunks, uint32_t sublen, hipStream_t st);
 template <typename T>
 int launch_brick_decode(const BrickLaunch& L, const uint32_t* bitstream, size_t bs_words, const uint8_t* revbook,
                         int bklen, const uint32_t* par_nbit, const uint32_t* par_entry, T* out, double eb, int radius,

@@ -98,6 +98,7 @@ struct Pipeline {
   size_t spl_x_words = 0;
   int sublen = 256, pardeg = 1;
   int user_sublen = 0;
+  int tuned_sublen = 256;  // tune_chunking's choice for this field
   int decoder = 0;  // PSZ_AMD_DECODER_*
   int last_layout = 1;   // layout of the last compress (PSZ_AMD_LAYOUT_*)
   int pack_reverse = 1;  // pass 2 walks bricks last-to-first (reuses pass 1's cache tail)
@@ -201,6 +202,7 @@ struct Pipeline {
     stream = (hipStream_t)st;
     CUSZ_AMD_HIP_CHECK(hipGetDevice(&device));
     tune_chunking(n, device, &sublen, &pardeg);
+    tuned_sublen = sublen;
     geom = lorenzo_geom(ndim, l.x, l.y, l.z, elem_bytes);
     if (ndim == 1) {
       // per-unit first cell + unsorted word: units of 16384 (reconstruction) or 256 (brick chunks)
@@ -355,8 +357,9 @@ struct Pipeline {
     if (radius < 1 || bklen > kMaxBklen) return PSZ_ABORT_NOT_IMPLEMENTED;
 
     const bool brick = use_brick(pred);
-    if (user_sublen && !brick) {
-      int s = std::min(8192, ((user_sublen + 255) / 256) * 256);
+    // chunk length: the caller's, else the tuned one
+    if (!brick) {
+      const int s = user_sublen ? std::min(8192, ((user_sublen + 255) / 256) * 256) : tuned_sublen;
       if (s != sublen) {
         sublen = s;
         pardeg = (int)((n - 1) / s + 1);
@@ -651,6 +654,16 @@ struct Pipeline {
     const size_t rvbk = rvbk_bytes(bklen);
     const int pd = h->vle_pardeg, sl = h->vle_sublen;
     const uint8_t* phf = in + phf_off;
+    if (sl % 64 == 0 && sl <= 8192 && decoder == 0 && pd > 0 && bklen <= kMaxBklen) {  // the fused decoders' chunk loop
+      const size_t bits_off = phf_off + 128 + rvbk + 8 * (size_t)pd;
+      const size_t total = h->entry[PSZHEADER_ENC_PASS2_END];
+      const size_t bs_words = total > bits_off ? (total - bits_off) / 4 : 0;
+      CUSZ_AMD_HIP_CHECK((hipError_t)launch_chunk_decode(
+          bl, reinterpret_cast<const uint32_t*>(phf + 128 + rvbk + 8 * (size_t)pd), bs_words, phf + 128, bklen,
+          reinterpret_cast<const uint32_t*>(phf + 128 + rvbk), reinterpret_cast<const uint32_t*>(phf + 128 + rvbk + 4 * (size_t)pd),
+          d_codes, n, (uint32_t)pd, (uint32_t)sl, stream));
+      return PSZ_SUCCESS;
+    }
     HfDecodeArgs da{reinterpret_cast<const uint32_t*>(phf + 128 + rvbk + 8 * (size_t)pd),
                     phf + 128,
                     bklen,
