@@ -1265,19 +1265,35 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
   const uint32_t ry = (uint32_t)lane >> 3, rz = (uint32_t)lane & 7u;
 
   BPROF(unsigned long long pc[16] = {}; unsigned long long tk = __builtin_readcyclecounter(), tp = tk;)
+  // A brick's chunk sizes / offsets and cell range are loaded during the previous brick's last
+  // block (they land while it decodes), so a brick starts with the bitstream loads only.
+  struct Next {
+    uint32_t nbit, entry, cb, ce;
+  };
+  auto fetch = [&](uint32_t b) {
+    Next x{0, 0, 0, 0};
+    if (b >= nbricks) return x;
+    const uint32_t bx = b % nbx, t = b / nbx, by = t % nby, bz = t / nby;
+    if (by * 8 + ry < ly && bz * 8 + rz < lz) {
+      const size_t c = ((size_t)(bz * 8 + rz) * ly + (by * 8 + ry)) * nbx + bx;
+      x.nbit = par_nbit[c], x.entry = par_entry[c];
+    }
+    if (ranked && ol.ncell) x.cb = ol.bstart[b], x.ce = ol.bstart[b + 1];
+    return x;
+  };
+  Next nx = fetch(blockIdx.x * (blockDim.x >> 6) + wid);
   for (uint32_t brick = blockIdx.x * (blockDim.x >> 6) + wid; brick < nbricks; brick += nw) {
     BPROF(pc[0]++; tp = __builtin_readcyclecounter();)
     const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
     const uint32_t y0 = by * 8, z0 = bz * 8;
     const bool live = y0 + ry < ly && z0 + rz < lz;
-    const size_t c = ((size_t)(z0 + rz) * ly + (y0 + ry)) * nbx + bx;
-    const uint32_t nbit = live ? par_nbit[c] : 0u;
-    const uint32_t vbase = (live ? par_entry[c] : 0u) * 4u;
+    const Next cur = nx;
+    const uint32_t nbit = live ? cur.nbit : 0u;
+    const uint32_t vbase = (live ? cur.entry : 0u) * 4u;
     // the brick's outlier cells [cb, ce): per-row counts -> row starts; values into LDS
     auto pro = [&]() {
       if (!ranked) return;
-      uint32_t cb = 0, ce = 0;
-      if (ol.ncell) cb = ol.bstart[brick], ce = ol.bstart[brick + 1];
+      const uint32_t cb = cur.cb, ce = cur.ce;
       const uint32_t nc = ce - cb;
       bc.row_start[lane] = 0;
       hfd::wave_sync();
@@ -1304,7 +1320,10 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
       else
         recon_block<T, ZZ, BUF, kTP, false>(tile, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane);
     };
-    decode_chunks(tb, rg, dw, live, vbase, nbit, W, pro, [](int) {}, recon BPROF_A);
+    auto blk_start = [&](int blk) {
+      if (blk == (int)(W / kBlk) - 1) nx = fetch(brick + nw);
+    };
+    decode_chunks(tb, rg, dw, live, vbase, nbit, W, pro, blk_start, recon BPROF_A);
   }
 #ifdef CUSZ_AMD_DEC_PROFILE
   if (lane == 0)
