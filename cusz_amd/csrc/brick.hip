@@ -1129,14 +1129,21 @@ template <class Pro, class BlkStart, class Recon>
 __device__ __forceinline__ void decode_chunks(const hfd::LdsTables<kDecB>& tb, const hfd::DecRegs& rg,
                                               const DecWave& dw, bool live, uint32_t vbase, uint32_t nbit,
                                               uint32_t vlen, Pro&& pro, BlkStart&& blk_start,
-                                              Recon&& recon BPROF_P, uint32_t W = 256)
+                                              Recon&& recon BPROF_P, uint32_t W = 256,
+                                              const u32x4* first = nullptr)
 {
   const int lane = dw.lane;
   uint32_t* ring_lane = dw.ring_lane;
   const uint32_t nwords = (nbit + 31u) >> 5;
-  // words 0..7 (0..2 into registers, 2..7 into the ring), issued before pro()
-  const u32x4 a0 = __builtin_amdgcn_raw_buffer_load_b128(dw.rbits, (int)(live ? vbase : kOOB), 0, 0);
-  const u32x4 a1 = __builtin_amdgcn_raw_buffer_load_b128(dw.rbits, (int)(live ? vbase + 16u : kOOB), 0, 0);
+  // words 0..7 (0..2 into registers, 2..7 into the ring): loaded by the caller ahead of time
+  // (first[0..1]), or now, before pro()
+  u32x4 a0, a1;
+  if (first)
+    a0 = first[0], a1 = first[1];
+  else {
+    a0 = __builtin_amdgcn_raw_buffer_load_b128(dw.rbits, (int)(live ? vbase : kOOB), 0, 0);
+    a1 = __builtin_amdgcn_raw_buffer_load_b128(dw.rbits, (int)(live ? vbase + 16u : kOOB), 0, 0);
+  }
   pro();
   uint32_t w0 = 0, w1 = a0.x, w2 = a0.y, nx = a0.z;
   ring_lane[2 * 64] = a0.z;  // nx is re-read every step, also by a first step that does not move
@@ -1267,21 +1274,37 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
   BPROF(unsigned long long pc[16] = {}; unsigned long long tk = __builtin_readcyclecounter(), tp = tk;)
   // A brick's chunk sizes / offsets and cell range are loaded during the previous brick's last
   // block (they land while it decodes), so a brick starts with the bitstream loads only.
+  // Its first bitstream words and first two outlier cells per lane are loaded at the start of
+  // the previous brick's last reconstruction (they land under its stores).
   struct Next {
     uint32_t nbit, entry, cb, ce;
+    bool live;
   };
   auto fetch = [&](uint32_t b) {
-    Next x{0, 0, 0, 0};
+    Next x{0, 0, 0, 0, false};
     if (b >= nbricks) return x;
     const uint32_t bx = b % nbx, t = b / nbx, by = t % nby, bz = t / nby;
-    if (by * 8 + ry < ly && bz * 8 + rz < lz) {
+    x.live = by * 8 + ry < ly && bz * 8 + rz < lz;
+    if (x.live) {
       const size_t c = ((size_t)(bz * 8 + rz) * ly + (by * 8 + ry)) * nbx + bx;
       x.nbit = par_nbit[c], x.entry = par_entry[c];
     }
     if (ranked && ol.ncell) x.cb = ol.bstart[b], x.ce = ol.bstart[b + 1];
     return x;
   };
+  u32x4 first[2];
+  uint2 pcell[2];  // cells cb + lane and cb + 64 + lane of the next brick: {value, index}
+  auto prefetch = [&](const Next& x) {
+    first[0] = __builtin_amdgcn_raw_buffer_load_b128(dw.rbits, (int)(x.live ? x.entry * 4u : kOOB), 0, 0);
+    first[1] = __builtin_amdgcn_raw_buffer_load_b128(dw.rbits, (int)(x.live ? x.entry * 4u + 16u : kOOB), 0, 0);
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const uint32_t j = x.cb + (uint32_t)lane + 64u * k;
+      pcell[k] = ranked && j < x.ce ? make_uint2(ol.cells[2 * (size_t)j], ol.cells[2 * (size_t)j + 1]) : make_uint2(0, 0);
+    }
+  };
   Next nx = fetch(blockIdx.x * (blockDim.x >> 6) + wid);
+  prefetch(nx);
   for (uint32_t brick = blockIdx.x * (blockDim.x >> 6) + wid; brick < nbricks; brick += nw) {
     BPROF(pc[0]++; tp = __builtin_readcyclecounter();)
     const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
@@ -1290,6 +1313,8 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
     const Next cur = nx;
     const uint32_t nbit = live ? cur.nbit : 0u;
     const uint32_t vbase = (live ? cur.entry : 0u) * 4u;
+    const u32x4 f2[2] = {first[0], first[1]};
+    const uint2 cp[2] = {pcell[0], pcell[1]};
     // the brick's outlier cells [cb, ce): per-row counts -> row starts; values into LDS
     auto pro = [&]() {
       if (!ranked) return;
@@ -1298,10 +1323,13 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
       bc.row_start[lane] = 0;
       hfd::wave_sync();
       for (uint32_t j = (uint32_t)lane; j < nc; j += 64) {
-        const uint32_t idx = ol.cells[2 * (cb + j) + 1];
+        const uint2 cell = j < 64u    ? cp[0]
+                           : j < 128u ? cp[1]
+                                      : make_uint2(ol.cells[2 * (size_t)(cb + j)], ol.cells[2 * (size_t)(cb + j) + 1]);
+        const uint32_t idx = cell.y;
         const uint32_t yz = idx / lx;  // y + ly z
         atomicAdd(&bc.row_start[((yz % ly) & 7u) * 8u + ((yz / ly) & 7u)], 1u);
-        if (nc <= kCellCap) cval[j] = ol.cells[2 * (cb + j)];
+        if (nc <= kCellCap) cval[j] = cell.x;
       }
       hfd::wave_sync();
       const uint32_t cr = bc.row_start[lane];
@@ -1313,6 +1341,7 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
       bc.vstride = nc <= kCellCap ? 1u : 2u;
     };
     auto recon = [&](int blk) {
+      if (blk == (int)(W / kBlk) - 1) prefetch(nx);  // the next brick (fetched during this block)
       const uint32_t nyv = min(8u, ly - y0), nzv = min(8u, lz - z0);
       const size_t base_elem = (size_t)z0 * plane + (size_t)y0 * lx + (size_t)bx * W + (size_t)blk * kBlk;
       if (ranked)
@@ -1323,7 +1352,7 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
     auto blk_start = [&](int blk) {
       if (blk == (int)(W / kBlk) - 1) nx = fetch(brick + nw);
     };
-    decode_chunks(tb, rg, dw, live, vbase, nbit, W, pro, blk_start, recon BPROF_A);
+    decode_chunks(tb, rg, dw, live, vbase, nbit, W, pro, blk_start, recon BPROF_A, W, f2);
   }
 #ifdef CUSZ_AMD_DEC_PROFILE
   if (lane == 0)
@@ -1374,6 +1403,21 @@ k_brick1_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
       const_cast<uint32_t*>(ol.cells), 0, (int)min(ol.ncell * 8, (size_t)0x7FFFFFFF), (int)kBufRsrcW3);
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
   BPROF(unsigned long long pc[16] = {}; unsigned long long tk = __builtin_readcyclecounter(), tp = tk;)
+  // chunk size / offset and cell range of each phase's chunk, loaded during the previous phase's
+  // last block (they land while it decodes)
+  struct Next {
+    uint32_t nbit, entry, cb, ce;
+  };
+  auto fetch = [&](uint32_t u, uint32_t p) {
+    Next x{0, 0, 0, 0};
+    const size_t c = ((size_t)u * 64u + (uint32_t)lane) * 4u + p;
+    if (u < nunits && c < nchunks) {
+      x.nbit = par_nbit[c], x.entry = par_entry[c];
+      if (ranked && ol.ncell) x.cb = ol.bstart[c], x.ce = ol.bstart[c + 1];
+    }
+    return x;
+  };
+  Next nxt = fetch(blockIdx.x * (blockDim.x >> 6) + wid, 0);
   for (uint32_t u = blockIdx.x * (blockDim.x >> 6) + wid; u < nunits; u += nw) {
     T carry = T(0);  // serial sum of this tile's segment totals (exclusive)
     T fh[16];        // raw thread totals of the current segment's first half
@@ -1386,15 +1430,17 @@ k_brick1_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
       BPROF(pc[0]++; tp = __builtin_readcyclecounter();)
       const size_t c = ((size_t)u * 64u + (uint32_t)lane) * 4u + p;
       const bool live = c < nchunks;
-      const uint32_t nbit = live ? par_nbit[c] : 0u;
-      const uint32_t vbase = (live ? par_entry[c] : 0u) * 4u;
+      const Next me = nxt;
+      const uint32_t nbit = live ? me.nbit : 0u;
+      const uint32_t vbase = (live ? me.entry : 0u) * 4u;
       const uint32_t vlen = live ? (uint32_t)min((size_t)256, n - c * 256u) : 0u;
       uint32_t cur = 0, cend = 0;  // this chunk's cells [cur, cend), cur advancing
       u32x4 pf[kCellPf / 2];
       auto pro = [&]() {
-        if (ranked && live && ol.ncell) cur = ol.bstart[c], cend = ol.bstart[c + 1];
+        if (ranked && live && ol.ncell) cur = me.cb, cend = me.ce;
       };
-      auto blk_start = [&](int) {
+      auto blk_start = [&](int blk) {
+        if (blk == (int)(256 / kBlk) - 1) nxt = p < 3 ? fetch(u, p + 1) : fetch(u + nw, 0);
         if (!ranked) return;
 #pragma unroll
         for (int h = 0; h < (int)kCellPf / 2; h++)
