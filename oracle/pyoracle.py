@@ -88,6 +88,8 @@ def ref():
         R.ref_build_codebook_u2.restype = C.c_int
         R.ref_build_codebook_u2.argtypes = [_P, C.c_int, _P, _P]
         R.ref_time_stages_f32.argtypes = [_P, _SZ, _SZ, _SZ, C.c_double, C.c_uint16, _P]
+        R.ref_time_stages_par_f32.argtypes = [_P, C.c_int, _P, _P, C.c_double, C.c_uint16, _P]
+        R.ref_time_stages_par_f32.restype = C.c_double
         _ref = R
     return _ref
 
@@ -308,3 +310,15 @@ def ref_time_stages(data, dims, eb, radius=512):
     ms = np.zeros(4, np.float64)
     ref().ref_time_stages_f32(_ptr(data), dims[0], dims[1], dims[2], eb, radius, _ptr(ms))
     return dict(c_lorenzo=ms[0], histogram=ms[1], codebook=ms[2], x_lorenzo=ms[3])
+
+
+def ref_time_stages_par(data, slabs, eb, radius=512):
+    """slabs: [(offset, (x, y, z))]; one thread per slab, stage clocks started together
+    (ref_shim.cc ref_time_stages_par_f32) -> (per-slab stage dicts, wall ms)."""
+    data = np.ascontiguousarray(data, np.float32)
+    off = np.array([o for o, _ in slabs], np.uint64)
+    dims = np.array([d for _, d in slabs], np.uint64).reshape(-1)
+    ms = np.zeros(4 * len(slabs), np.float64)
+    wall = ref().ref_time_stages_par_f32(_ptr(data), len(slabs), _ptr(off), _ptr(dims), eb, radius, _ptr(ms))
+    return [dict(c_lorenzo=ms[4 * i], histogram=ms[4 * i + 1], x_lorenzo=ms[4 * i + 3])
+            for i in range(len(slabs))], wall

@@ -18,6 +18,10 @@
 //   psz::module::CPU_scatter<f4,u4>::kernel_v2                        psz/src/kernel/spvn.seq.cc:19-29
 
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
+#include <vector>
 #include <cstdint>
 #include <cstring>
 #include <memory>
@@ -136,54 +140,126 @@ int ref_build_codebook_u2(const uint32_t* hist, int bklen, uint32_t* book, uint8
   return rvbk_bytes;
 }
 
-// Timing helper for the CPU baseline leg: reference CPU compress stages on a
-// 3D field, single thread.  Returns milliseconds per stage in ms[0..3]:
-// c_lorenzo, histogram, codebook, x_lorenzo.
+// Timing helpers for the CPU baseline leg: the reference CPU compress stages (c_lorenzo,
+// histogram, codebook, x_lorenzo) on one field, milliseconds per stage in ms[0..3].  Every
+// buffer is allocated and zeroed before the stage clocks start.
+}  // extern "C"
+
+namespace {
+
+struct StageRun {
+  size_t x, y, z, n, npad;
+  std::unique_ptr<uint16_t[]> codes;
+  std::unique_ptr<_portable::compact_CPU<f4, u4>> outlier;
+  std::unique_ptr<uint32_t[]> hist, book;
+  std::unique_ptr<uint8_t[]> revbook;
+  std::unique_ptr<float[]> xdata;
+  int rvbk_bytes;
+  uint16_t radius;
+
+  StageRun(size_t x_, size_t y_, size_t z_, uint16_t radius_) : x(x_), y(y_), z(z_), radius(radius_)
+  {
+    n = x * y * z;
+    // The reference predicts every point of a partial tile, stale buffer contents included, and
+    // may record outliers at indices past the field (lrz.seq.inl:266-284: no boundary check
+    // before the outlier append); CPU_scatter then writes them.  Size the outlier list and the
+    // scatter target for the largest such index (x < 256-, y < 16-, z < 8-multiples).
+    auto up = [](size_t v, size_t m) { return (v + m - 1) / m * m; };
+    const size_t ry = y == 1 ? 1 : up(y, 16), rz = z == 1 ? 1 : up(z, 8);
+    npad = up(x, 256) + ry * x + rz * x * y;
+    codes = std::make_unique<uint16_t[]>(n);
+    memset(codes.get(), 0, sizeof(uint16_t) * n);  // pages faulted in before the clocks
+    outlier = std::make_unique<_portable::compact_CPU<f4, u4>>(npad);
+    hist = std::make_unique<uint32_t[]>(2 * radius);
+    book = std::make_unique<uint32_t[]>(2 * radius);
+    rvbk_bytes = (int)phf_reverse_book_bytes(2 * radius, 4, sizeof(u2));
+    revbook = std::make_unique<uint8_t[]>(rvbk_bytes);
+    xdata = std::make_unique<float[]>(npad);
+    memset(hist.get(), 0, sizeof(uint32_t) * 2 * radius);
+    memset(xdata.get(), 0, sizeof(float) * npad);
+  }
+
+  // c_lorenzo, histogram, codebook; then the outlier scatter (untimed) and x_lorenzo
+  void run(const float* in, double eb, double* ms, bool with_book)
+  {
+    using clk = std::chrono::steady_clock;
+    auto ms_since = [](clk::time_point t0) {
+      return std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    };
+    psz_len len{x, y, z};
+    auto t0 = clk::now();
+    psz::module::CPU_c_lorenzo_nd_with_outlier<f4, false, u2>::kernel(
+        const_cast<float*>(in), len, codes.get(), outlier.get(), eb, radius, nullptr);
+    ms[0] = ms_since(t0);
+    t0 = clk::now();
+    psz::module::SEQ_histogram_generic<u2>(codes.get(), n, hist.get(), 2 * radius, nullptr);
+    ms[1] = ms_since(t0);
+    ms[2] = 0;
+    if (with_book) {
+      t0 = clk::now();
+      phf_CPU_build_canonized_codebook_v2<u2, u4>(
+          hist.get(), 2 * radius, book.get(), revbook.get(), rvbk_bytes, nullptr);
+      ms[2] = ms_since(t0);
+    }
+    psz::module::CPU_scatter<f4, u4>::kernel_v2(outlier->val_idx(), outlier->num(), xdata.get());
+    t0 = clk::now();
+    psz::module::CPU_x_lorenzo_nd<f4, false, u2>::kernel(
+        codes.get(), xdata.get(), xdata.get(), len, eb, radius, nullptr);
+    ms[3] = ms_since(t0);
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
 void ref_time_stages_f32(
     const float* in, size_t x, size_t y, size_t z, double eb, uint16_t radius, double* ms)
 {
-  size_t n = x * y * z;
-  // The reference predicts every point of a partial tile, stale buffer contents included, and
-  // may record outliers at indices past the field (lrz.seq.inl:266-284: no boundary check before
-  // the outlier append); CPU_scatter then writes them.  Size the outlier list and the scatter
-  // target for the largest such index (x < 256-, y < 16-, z < 8-multiples) so it stays in bounds.
-  auto up = [](size_t v, size_t m) { return (v + m - 1) / m * m; };
-  const size_t ry = y == 1 ? 1 : up(y, 16), rz = z == 1 ? 1 : up(z, 8);
-  const size_t npad = up(x, 256) + ry * x + rz * x * y;
-  auto codes = std::make_unique<uint16_t[]>(n);
-  auto outlier = std::make_unique<_portable::compact_CPU<f4, u4>>(npad);
-  auto hist = std::make_unique<uint32_t[]>(2 * radius);
-  auto book = std::make_unique<uint32_t[]>(2 * radius);
-  int rvbk_bytes = (int)phf_reverse_book_bytes(2 * radius, 4, sizeof(u2));
-  auto revbook = std::make_unique<uint8_t[]>(rvbk_bytes);
-  auto xdata = std::make_unique<float[]>(npad);
-  psz_len len{x, y, z};
-  using clk = std::chrono::steady_clock;
-  auto ms_since = [](clk::time_point t0) {
-    return std::chrono::duration<double, std::milli>(clk::now() - t0).count();
-  };
+  StageRun r(x, y, z, radius);
+  r.run(in, eb, ms, true);
+}
 
-  auto t0 = clk::now();
-  psz::module::CPU_c_lorenzo_nd_with_outlier<f4, false, u2>::kernel(
-      const_cast<float*>(in), len, codes.get(), outlier.get(), eb, radius, nullptr);
-  ms[0] = ms_since(t0);
-
-  memset(hist.get(), 0, sizeof(uint32_t) * 2 * radius);
-  t0 = clk::now();
-  psz::module::SEQ_histogram_generic<u2>(codes.get(), n, hist.get(), 2 * radius, nullptr);
-  ms[1] = ms_since(t0);
-
-  t0 = clk::now();
-  phf_CPU_build_canonized_codebook_v2<u2, u4>(
-      hist.get(), 2 * radius, book.get(), revbook.get(), rvbk_bytes, nullptr);
-  ms[2] = ms_since(t0);
-
-  memset(xdata.get(), 0, sizeof(float) * npad);
-  psz::module::CPU_scatter<f4, u4>::kernel_v2(outlier->val_idx(), outlier->num(), xdata.get());
-  t0 = clk::now();
-  psz::module::CPU_x_lorenzo_nd<f4, false, u2>::kernel(
-      codes.get(), xdata.get(), xdata.get(), len, eb, radius, nullptr);
-  ms[3] = ms_since(t0);
+// All-core variant: slab s (element offset off[s], dims dims[3s..3s+2]) on its own thread.
+// Every thread allocates and zeroes its buffers, then all start the stage clocks together
+// (barrier) and free nothing until all are done, so no thread's mmap/munmap or page faults
+// stall another's timed stages.  ms[4s..4s+3] per slab; returns the wall time in ms of the
+// concurrent region (the slowest thread's c_lorenzo + histogram + scatter + x_lorenzo).
+double ref_time_stages_par_f32(
+    const float* in, int nslab, const size_t* off, const size_t* dims, double eb, uint16_t radius,
+    double* ms)
+{
+  std::vector<std::unique_ptr<StageRun>> runs(nslab);
+  std::mutex mu;
+  std::condition_variable cv;
+  int ready = 0, done = 0;
+  std::chrono::steady_clock::time_point t0, t1;
+  std::vector<std::thread> th;
+  for (int s = 0; s < nslab; s++)
+    th.emplace_back([&, s] {
+      runs[s] = std::make_unique<StageRun>(dims[3 * s], dims[3 * s + 1], dims[3 * s + 2], radius);
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        if (++ready == nslab) {
+          t0 = std::chrono::steady_clock::now();
+          cv.notify_all();
+        }
+        else
+          cv.wait(lk, [&] { return ready == nslab; });
+      }
+      runs[s]->run(in + off[s], eb, ms + 4 * s, false);
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        if (++done == nslab) {
+          t1 = std::chrono::steady_clock::now();
+          cv.notify_all();
+        }
+        else
+          cv.wait(lk, [&] { return done == nslab; });
+      }
+    });
+  for (auto& t : th) t.join();
+  return std::chrono::duration<double, std::milli>(t1 - t0).count();
 }
 
 }  // extern "C"
