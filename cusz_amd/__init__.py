@@ -98,7 +98,8 @@ EXPORTS = [
     "phf_version", "phf_versioninfo",
     # cusz_amd.h
     "psz_amd_get_internals", "psz_amd_enable_timing", "psz_amd_stage_times", "psz_amd_set_sublen",
-    "psz_amd_decode_codes", "psz_amd_set_decoder", "psz_amd_set_layout", "psz_amd_version",
+    "psz_amd_decode_codes", "psz_amd_set_decoder", "psz_amd_set_layout", "psz_amd_set_codebook",
+    "psz_amd_version",
     "psz_amd_compress_scan_float", "psz_amd_compress_scan_double", "psz_amd_compress_finish",
     "psz_amd_merge_archives", "psz_amd_value_range",
 ]
@@ -142,6 +143,7 @@ def lib():
     L.psz_amd_decode_codes.argtypes = [P, P]
     L.psz_amd_set_decoder.argtypes = [P, C.c_int]
     L.psz_amd_set_layout.argtypes = [P, C.c_int]
+    L.psz_amd_set_codebook.argtypes = [P, C.c_int]
     L.psz_amd_version.restype = C.c_char_p
     for fn in (L.psz_amd_compress_scan_float, L.psz_amd_compress_scan_double):
         fn.restype = C.c_int
@@ -166,6 +168,7 @@ def lib():
 DECODER_AUTO, DECODER_LANE, DECODER_WAVE = 0, 1, 2
 # archive layout (PSZ_AMD_LAYOUT_*)
 LAYOUT_BRICK, LAYOUT_REFERENCE = 0, 1
+CODEBOOK_EXACT, CODEBOOK_SAMPLED = 0, 1
 
 
 class PszError(RuntimeError):
@@ -275,6 +278,13 @@ class Resource:
         st = lib().psz_amd_set_layout(self._h, int(layout))
         if st != PSZ_SUCCESS:
             raise PszError(st, "psz_amd_set_layout")
+
+    def set_codebook(self, mode: int):
+        """CODEBOOK_EXACT (full histogram, default) or CODEBOOK_SAMPLED (every 16th brick's
+        histogram + 1, one predict+pack pass; 3-D brick fields only)."""
+        st = lib().psz_amd_set_codebook(self._h, int(mode))
+        if st != PSZ_SUCCESS:
+            raise PszError(st, "psz_amd_set_codebook")
 
     def decode_codes(self, d_archive: int):
         st = lib().psz_amd_decode_codes(self._h, C.c_void_p(d_archive))

@@ -287,6 +287,7 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
   constexpr int D = kScanAhead<T>;
   static_assert(64 % D == 0 && D % 8 == 0, "the queue holds whole y-steps");
   uint32_t u = blockIdx.x * kBrickWaves + wid;
+  const T bias = r - (T)bcs.c0;  // the byte-first path (below)
   T q[D][V];
 #pragma unroll
   for (int j = 0; j < D; j++) ld.issue_row(u * kUnitBricks, j, q[j]);
@@ -303,6 +304,10 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
       uint8_t* cbrick8 = bcs.c8 + (size_t)brick * 64 * (64 * V) + (size_t)lane * V;
       rowmask = 0;
       T bprev[8][V], pprev[V];
+#pragma unroll
+      for (int z = 0; z < 8; z++)
+#pragma unroll
+        for (int k = 0; k < V; k++) bprev[z][k] = (T)0;
 #pragma unroll 1
       for (int r0 = 0; r0 < 64; r0 += D)  // not unrolled: instruction cache
 #pragma unroll
@@ -328,21 +333,56 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
           T d[V];
 #pragma unroll
           for (int k = 0; k < V; k++) {
-            d[k] = y > 0 ? a[k] - bprev[z][k] : a[k];
+            d[k] = a[k] - bprev[z][k];  // bprev = 0 on the brick's first y-step: a - 0 == a
             bprev[z][k] = a[k];
           }
           if (gy >= ly || z0 + (uint32_t)z >= lz) continue;  // outside the field (wave-uniform)
           float olv[V];
           uint16_t qc[V];
           uint64_t anyol = 0;  // SALU: OR of the per-element outlier lane masks
+          if constexpr (!ZZ && sizeof(T) == 4 && kHistCopies == 1) {
+            // Byte-first quantization.  d is integer-valued, so for |d| < r the reference code
+            // (int)(d + r) equals (int)(d + bias) + c0 (bias = r - c0, i.e. 127 unless r < 127) and
+            // the byte is (int)(d + bias).
+            // A row is clean when every element has |d| < r and a byte in [0, 254]: then the
+            // bytes pack by shifts, the histogram bin is byte + c0, and nothing else is computed.
+            // Any other row (an outlier, a NaN, a code outside the byte window) takes the exact path.
+            int cib[V];
+            bool q[V];
+            uint64_t suspect = 0;
 #pragma unroll
-          for (int k = 0; k < V; k++) {
-            bool is_ol;
-            qc[k] = quantize<T, ZZ>(d[k], r, is_ol, olv[k]);
-            anyol |= __ballot(is_ol);
+            for (int k = 0; k < V; k++) {
+              cib[k] = (int)(d[k] + bias);
+              q[k] = dabs(d[k]) < r;
+              anyol |= __ballot(!q[k]);
+              suspect |= __ballot((uint32_t)cib[k] > 254u);
+            }
+            if ((suspect | anyol) == 0) {
+              uint32_t* s_hc0 = s_hist + bcs.c0;
+#pragma unroll
+              for (int k = 0; k < V; k++) atomicAdd(&s_hc0[cib[k]], 1u);
+              static_assert(V == 4, "one 4-B byte store per lane and row");
+              *reinterpret_cast<uint32_t*>(cbrick8 + (size_t)row * (64 * V)) =
+                  (uint32_t)cib[0] | (uint32_t)cib[1] << 8 | (uint32_t)cib[2] << 16 | (uint32_t)cib[3] << 24;
+              continue;
+            }
+#pragma unroll
+            for (int k = 0; k < V; k++) {
+              qc[k] = q[k] ? (uint16_t)(cib[k] + (int)bcs.c0) : uint16_t(0);
+              olv[k] = (float)(d[k] + r);  // quantize(): the outlier value is d + r
+              atomicAdd(&s_hist[qc[k]], 1u);
+            }
+          }
+          else {
+#pragma unroll
+            for (int k = 0; k < V; k++) {
+              bool is_ol;
+              qc[k] = quantize<T, ZZ>(d[k], r, is_ol, olv[k]);
+              anyol |= __ballot(is_ol);
 #ifndef CUSZ_AMD_SCAN_NOHIST  // (timing experiment switch: no histogram)
-            atomicAdd(&s_hist[qc[k] * kHistCopies + hc], 1u);
+              atomicAdd(&s_hist[qc[k] * kHistCopies + hc], 1u);
 #endif
+            }
           }
 #ifndef CUSZ_AMD_SCAN_NOCODES  // (timing experiment switch: no code stores)
           store_brick_row<V>(bcs, cbrick, cbrick8, row, qc, rowmask);
@@ -1725,6 +1765,328 @@ k_chunk_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const 
   }
 }
 
+
+// =========================================================================================
+// sampled-codebook mode: one pass predicts and packs (psz_amd_set_codebook(SAMPLED))
+// =========================================================================================
+// The codebook is built from the histogram of every kSampleStride-th brick, +1 on every bin so
+// every code is encodable, BEFORE the field is predicted.  One pass then predicts a brick, keeps
+// its codes in LDS (byte rows; a row with a code outside the byte window goes to global memory as
+// u16), learns its exact size in cells, takes its archive offset by a decoupled look-back over
+// the bricks before it and packs the rows straight into the archive: the codes never travel
+// through HBM and no plan pass runs.  Bricks are claimed in order from a ticket, so every brick a
+// look-back waits on is held by a running wave (the smallest unfinished brick never waits).
+// Codes, outliers and the reconstruction are the exact mode's; the codebook, hence the
+// bitstream, differs (chunks back to back, no gaps).
+constexpr uint32_t kSampleStride = 16;
+constexpr unsigned long long kStAgg = 1ull << 62, kStInc = 2ull << 62;  // look-back status flags
+
+// pass 0: the histogram of bricks 0, stride, 2 stride, ... (prediction as pass 1)
+template <typename T, bool ZZ>
+__global__ void __launch_bounds__(64 * kBrickWaves)
+k_brick3_sample(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T ebx2_r, T r,
+                uint32_t* __restrict__ g_hist, int bklen, uint32_t nbx, uint32_t nby, uint32_t nbricks,
+                uint32_t stride)
+{
+  __shared__ uint32_t s_h[kMaxBklen];
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (int i = threadIdx.x; i < bklen; i += blockDim.x) s_h[i] = 0;
+  __syncthreads();
+  const StepLoader<T, 4> ld{in, (size_t)lx * ly, lx, ly, lz, nbx, nby, nbricks, 0, (uint32_t)lane};
+  const uint32_t nsamp = (nbricks + stride - 1) / stride;
+  for (uint32_t sidx = blockIdx.x * kBrickWaves + wid; sidx < nsamp; sidx += gridDim.x * kBrickWaves) {
+    const uint32_t brick = sidx * stride;
+    const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
+    const uint32_t x0 = bx * 256 + (uint32_t)lane * 4;
+    T bprev[8][4], raw[8][4], p[8][4];
+    ld.issue(brick, 0, raw);
+    for (int y = 0; y < 8; y++) {
+      prequant_ystep<T, 4>(raw, ebx2_r, p);
+      if (y + 1 < 8) ld.issue(brick, y + 1, raw);
+      residual_ystep<T, 4>(x0, y, bprev, p);
+      if (by * 8 + (uint32_t)y >= ly) break;
+#pragma unroll
+      for (int z = 0; z < 8; z++) {
+        if (bz * 8 + (uint32_t)z >= lz) break;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          bool ol;
+          float ov;
+          atomicAdd(&s_h[quantize<T, ZZ>(p[z][k], r, ol, ov)], 1u);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < bklen; i += blockDim.x)
+    if (s_h[i]) atomicAdd(&g_hist[i], s_h[i]);
+}
+
+__device__ __forceinline__ unsigned long long st_word(unsigned long long flag, uint32_t cells, uint32_t oc)
+{
+  return flag | (unsigned long long)cells | ((unsigned long long)oc << 32);
+}
+
+// Exclusive prefix (cells, slot outliers) of `brick` from its predecessors' status words: 64 at
+// a time, back to the nearest one holding an inclusive prefix (lane 0 = brick - 1).  Bounded
+// spins: a word still empty after them counts as 0 and raises *timeout (never expected).
+__device__ __forceinline__ void lookback(const unsigned long long* status, uint32_t brick, int lane, uint32_t& xc,
+                                         uint32_t& xo, unsigned int* timeout)
+{
+  uint32_t sc = 0, so = 0;
+  for (int64_t j = (int64_t)brick - 1;; j -= 64) {
+    const int64_t me = j - lane;
+    unsigned long long v = kStInc;  // before brick 0: an inclusive prefix of 0
+    if (me >= 0) {
+      uint32_t spins = 0;
+      do
+        v = __hip_atomic_load(status + me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while ((v >> 62) == 0 && ++spins < (1u << 22));
+      if ((v >> 62) == 0) atomicOr(timeout, 1u);
+    }
+    const uint64_t inc = __builtin_amdgcn_ballot_w64((v >> 62) == 2);
+    const int k = inc ? __builtin_ctzll(inc) : 64;
+    const bool take = lane <= k;
+    const uint32_t c = take ? (uint32_t)v : 0u, o = take ? (uint32_t)(v >> 32) & 0x3FFFFFFFu : 0u;
+    sc += readlane(hfd::wave_incl_scan(c), 63);
+    so += readlane(hfd::wave_incl_scan(o), 63);
+    if (inc) break;
+  }
+  xc = sc, xo = so;
+}
+
+struct SingleArgs {
+  uint32_t lx, ly, lz, nbx, nby, nbricks;
+  OutlierSink ol;
+  BrickCodes bcs;  // c16: the u16 rows (brick order); c0
+  const uint32_t* book;
+  int bklen;
+  uint32_t* par_nbit;
+  uint32_t* par_entry;
+  uint32_t* bitstream;
+  unsigned long long* status;  // per brick, zeroed per call
+  uint32_t* ticket;            // zeroed per call
+  uint32_t* ol_pre;            // per brick: exclusive prefix of slot outliers
+  CompressInfo* info;
+  unsigned int* timeout;
+};
+
+constexpr int kSingleWaveWords = 64 * 64 + pack_cells_words<4>();  // byte rows + packing cells
+
+template <typename T, bool ZZ>
+__global__ void __launch_bounds__(64 * kBrickWaves)
+k_brick3_single(const T* __restrict__ in, SingleArgs a, T ebx2_r, T r)
+{
+  constexpr int V = 4;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint32_t* s_book = smem;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t* rows8 = smem + kMaxBklen + wid * kSingleWaveWords;  // 64 byte rows of 256
+  uint32_t* cells = rows8 + 64 * 64;
+  for (int i = threadIdx.x; i < a.bklen; i += blockDim.x) s_book[i] = a.book[i];
+  for (int i = lane; i < pack_cells_words<V>(); i += 64) cells[i] = 0;
+  __syncthreads();
+  const StepLoader<T, V> ld{in, (size_t)a.lx * a.ly, a.lx, a.ly, a.lz, a.nbx, a.nby, a.nbricks, 0, (uint32_t)lane};
+  const size_t plane = ld.plane;
+  const uint32_t c0 = a.bcs.c0;
+  auto claim = [&]() -> uint32_t {
+    uint32_t b = 0;
+    if (lane == 0) b = atomicAdd(a.ticket, 1u);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
+  };
+  constexpr int D = kScanAhead<T>;
+  uint32_t brick = claim();
+  T q[D][V];
+#pragma unroll
+  for (int j = 0; j < D; j++) ld.issue_row(brick, j, q[j]);
+  while (brick < a.nbricks) {
+    const uint32_t bnext = claim();
+    const uint32_t bx = brick % a.nbx, t = brick / a.nbx, by = t % a.nby, bz = t / a.nby;
+    const uint32_t x0 = bx * (64 * V) + lane * V, y0 = by * 8, z0 = bz * 8;
+    const uint32_t nyv = min(8u, a.ly - y0), nzv = min(8u, a.lz - z0);
+    uint16_t* cbrick = a.bcs.c16 + (size_t)brick * 64 * (64 * V) + (size_t)lane * V;
+    uint64_t rowmask = 0;
+    uint32_t cnt = 0, bcells = 0;
+    unsigned long long bbits = 0;
+    T bprev[8][V], pprev[V];
+#pragma unroll
+    for (int z = 0; z < 8; z++)
+#pragma unroll
+      for (int k = 0; k < V; k++) bprev[z][k] = (T)0;
+    // phase 1: predict, codes into LDS (or u16 rows to global), outliers into the brick's slot
+#pragma unroll 1
+    for (int r0 = 0; r0 < 64; r0 += D)
+#pragma unroll
+      for (int j = 0; j < D; j++) {
+        const int row = r0 + j, z = j & 7, y = row >> 3;
+        T p[V];
+#pragma unroll
+        for (int k = 0; k < V; k++) p[k] = dround(q[j][k] * ebx2_r);
+        if (row + D < 64) ld.issue_row(brick, row + D, q[j]);
+        else ld.issue_row(bnext, row + D - 64, q[j]);
+        const uint32_t gy = y0 + (uint32_t)y;
+        T av[V];
+#pragma unroll
+        for (int k = 0; k < V; k++) {
+          av[k] = z > 0 ? p[k] - pprev[k] : p[k];
+          pprev[k] = p[k];
+        }
+        const T west = shr_in_tile<T, 1, 8 / V>(av[V - 1]);
+#pragma unroll
+        for (int k = V - 1; k > 0; k--) av[k] = av[k] - av[k - 1];
+        if (x0 % 8 != 0) av[0] = av[0] - west;
+        T d[V];
+#pragma unroll
+        for (int k = 0; k < V; k++) {
+          d[k] = av[k] - bprev[z][k];
+          bprev[z][k] = av[k];
+        }
+        if (gy >= a.ly || z0 + (uint32_t)z >= a.lz) continue;  // outside the field (wave-uniform)
+        float olv[V];
+        uint16_t qc[V];
+        uint64_t anyol = 0;
+        uint32_t bits = 0;
+        bool wide = false;
+#pragma unroll
+        for (int k = 0; k < V; k++) {
+          bool is_ol;
+          qc[k] = quantize<T, ZZ>(d[k], r, is_ol, olv[k]);
+          anyol |= __ballot(is_ol);
+          bits += s_book[qc[k]] >> 27;
+          wide |= (uint32_t)qc[k] - c0 > 254u && qc[k] != 0;
+        }
+        const uint32_t rb = readlane(hfd::wave_incl_scan(bits), 63);
+        bbits += rb;
+        bcells += (rb + 31u) >> 5;
+        if (__builtin_amdgcn_ballot_w64(wide)) {
+          store_codes_row<V>(cbrick + (size_t)row * (64 * V), qc);
+          rowmask |= 1ull << row;
+        }
+        else {
+          uint32_t w = 0;
+#pragma unroll
+          for (int k = 0; k < V; k++) w |= (qc[k] == 0 ? 255u : (uint32_t)qc[k] - c0) << (8 * k);
+          rows8[row * 64 + lane] = w;
+        }
+        if (anyol) {
+          uint32_t mask = 0;
+          size_t idx[V];
+          const size_t base = (size_t)(z0 + z) * plane + (size_t)gy * a.lx;
+#pragma unroll
+          for (int k = 0; k < V; k++) {
+            mask |= (uint32_t)(qc[k] == 0 && (ZZ ? !(dabs(d[k]) < r) : true)) << k;
+            idx[k] = base + x0 + k;
+          }
+          emit_outliers<V>(a.ol, brick, cnt, mask, olv, idx);
+        }
+      }
+    // the brick's place in the archive
+    const uint32_t oc = min(cnt, a.ol.cap_per_brick);
+    uint32_t xc = 0, xo = 0;
+    if (brick == 0) {
+      if (lane == 0) __hip_atomic_store(a.status, st_word(kStInc, bcells, oc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    else {
+      if (lane == 0) __hip_atomic_store(a.status + brick, st_word(kStAgg, bcells, oc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      lookback(a.status, brick, lane, xc, xo, a.timeout);
+      if (lane == 0)
+        __hip_atomic_store(a.status + brick, st_word(kStInc, xc + bcells, xo + oc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) {
+      a.ol.brick_cnt[brick] = cnt;
+      a.ol_pre[brick] = xo;
+      atomicAdd(&a.info->total_nbit, bbits);
+    }
+    hfd::wave_sync();
+    // phase 2: pack the rows (k_brick3_pack's row loop) at cell xc onwards, back to back; the
+    // u16 rows this wave stored are read back (their stores drained first)
+    if (rowmask) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t* dst = a.bitstream + xc;
+    uint32_t off = 0, my_nbit = 0, my_entry = 0;
+    for (uint32_t y = 0; y < nyv; y++)
+      for (uint32_t z = 0; z < nzv; z++) {
+        const uint32_t row = y * 8 + z;
+        uint32_t qs[4];
+        if ((rowmask >> row) & 1ull) {
+          uint2 v;
+          __builtin_memcpy(&v, cbrick + (size_t)row * (64 * V), 8);
+          qs[0] = v.x & 0xFFFFu, qs[1] = v.x >> 16, qs[2] = v.y & 0xFFFFu, qs[3] = v.y >> 16;
+        }
+        else {
+          const uint32_t w8 = rows8[row * 64 + lane];
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const uint32_t b = (w8 >> (8 * k)) & 255u;
+            qs[k] = b == 255u ? 0u : b + c0;
+          }
+        }
+        uint32_t w[V], bits = 0;
+#pragma unroll
+        for (int k = 0; k < V; k++) {
+          w[k] = s_book[qs[k]];
+          bits += w[k] >> 27;
+        }
+        const uint32_t inc = hfd::wave_incl_scan(bits);
+        const uint32_t tot = readlane(inc, 63);
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(bits > 64u) == 0, 1))
+          hfd::pack4_or(cells, inc - bits, w, bits);
+        else
+          hfd::pack_words<V>(cells, inc - bits, w, V);
+        hfd::wave_sync();
+        const uint32_t nc = (tot + 31) >> 5;
+        for (uint32_t i = lane; i < nc; i += 64) {
+          dst[off + i] = cells[i];
+          cells[i] = 0;
+        }
+        if ((uint32_t)lane == row) my_nbit = tot, my_entry = xc + off;
+        off += nc;
+        hfd::wave_sync();
+      }
+    const uint32_t ry = lane >> 3, rz = lane & 7;
+    if (ry < nyv && rz < nzv) {
+      const size_t c = ((size_t)(z0 + rz) * a.ly + (y0 + ry)) * a.nbx + bx;
+      a.par_nbit[c] = my_nbit;
+      a.par_entry[c] = my_entry;
+    }
+    brick = bnext;
+  }
+}
+
+// after the single pass: the outlier segment (slots in brick order, then the spill list), the
+// totals and both headers; the last workgroup publishes the compress summary
+__global__ void __launch_bounds__(256) k_brick3_single_finish(SingleArgs a, HeaderTpl tpl, uint8_t* archive,
+                                                              size_t phf_offset, size_t bits_rel, HostPub pub)
+{
+  const unsigned long long last =
+      __hip_atomic_load(a.status + a.nbricks - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t ncell = (uint32_t)last, slot_total = (uint32_t)(last >> 32) & 0x3FFFFFFFu;
+  uint2* ol_dst = reinterpret_cast<uint2*>(a.bitstream + ncell);
+  const uint32_t lane = threadIdx.x & 63, nwv = gridDim.x * 4;
+  for (uint32_t b = (blockIdx.x * 256 + threadIdx.x) >> 6; b < a.nbricks; b += nwv) {
+    const uint32_t cnt = min(a.ol.brick_cnt[b], a.ol.cap_per_brick);
+    const uint64_t* slot = a.ol.slots + (size_t)b * a.ol.cap_per_brick;
+    uint2* d = ol_dst + a.ol_pre[b];
+    for (uint32_t i = lane; i < cnt; i += 64) {
+      const uint64_t c = slot[i];
+      d[i] = make_uint2((uint32_t)c, (uint32_t)(c >> 32));
+    }
+  }
+  const uint32_t sp = *a.ol.spill_cnt, sp_kept = min(sp, a.ol.spill_cap);
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < sp_kept; i += gridDim.x * 256) {
+    const uint64_t c = a.ol.spill[i];
+    ol_dst[slot_total + i] = make_uint2((uint32_t)c, (uint32_t)(c >> 32));
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const unsigned long long nbit = __hip_atomic_load(&a.info->total_nbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    a.info->total_ncell = ncell;
+    a.info->splen = slot_total + sp_kept;
+    a.info->outlier_lost = sp > a.ol.spill_cap ? sp - a.ol.spill_cap : 0u;
+    write_headers_dev(archive, tpl, nbit, ncell, slot_total + sp_kept, phf_offset, bits_rel);
+    __threadfence();  // the header and totals reach memory before the ticket (the publisher may be another XCD)
+  }
+  publish_last(pub);
+}
+
 }  // namespace
 
 // =========================================================================================
@@ -1849,6 +2211,65 @@ int launch_brick_pack(const BrickLaunch& L, const BrickCodes& bcodes, const uint
                                                                     reverse, overflow, pub);
   return (int)hipGetLastError();
 }
+
+template <typename T>
+int launch_brick_sample(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, uint32_t* hist, int bklen,
+                        hipStream_t st)
+{
+  const BrickGeom& g = L.g;
+  if (g.ndim != 3) return (int)hipErrorInvalidValue;
+  const T ebx2_r = (T)(1.0 / (eb * 2)), r = (T)radius;
+  const uint32_t stride = g.nbricks >= 64 * kSampleStride ? kSampleStride : 1u;
+  const uint32_t nsamp = (g.nbricks + stride - 1) / stride;
+  const uint32_t grid = std::max(1u, std::min((nsamp + kBrickWaves - 1) / kBrickWaves, (uint32_t)L.ncu * 4));
+  if (zz)
+    k_brick3_sample<T, true><<<grid, 64 * kBrickWaves, 0, st>>>(in, L.lx, L.ly, L.lz, ebx2_r, r, hist, bklen, g.nbx,
+                                                                g.nby, g.nbricks, stride);
+  else
+    k_brick3_sample<T, false><<<grid, 64 * kBrickWaves, 0, st>>>(in, L.lx, L.ly, L.lz, ebx2_r, r, hist, bklen, g.nbx,
+                                                                 g.nby, g.nbricks, stride);
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+int launch_brick_single(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const BrickSingle& s,
+                        const void* psz_tpl, const void* phf_tpl, hipStream_t st, const HostPub& pub)
+{
+  const BrickGeom& g = L.g;
+  if (g.ndim != 3) return (int)hipErrorInvalidValue;
+  const T ebx2_r = (T)(1.0 / (eb * 2)), r = (T)radius;
+  SingleArgs a{L.lx, L.ly, L.lz, g.nbx, g.nby, g.nbricks, s.ol, s.bcs, s.book, s.bklen, s.par_nbit, s.par_entry,
+               s.bitstream, s.status, s.ticket, s.ol_pre, s.info, s.timeout};
+  const size_t lds = ((size_t)kMaxBklen + (size_t)kBrickWaves * kSingleWaveWords) * 4;
+  static int per_cu[2] = {0, 0};
+  int& pc = per_cu[sizeof(T) == 8];
+  if (!pc) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k_brick3_single<T, false>, 64 * kBrickWaves, lds) != hipSuccess ||
+        pc < 1)
+      pc = 1;
+  }
+  // persistent waves claim bricks from the ticket; every one must be resident (the look-back
+  // waits only on claimed bricks, and a claimed brick's wave is running)
+  const uint32_t grid = std::max(1u, std::min((g.nbricks + kBrickWaves - 1) / kBrickWaves, (uint32_t)(pc * L.ncu)));
+  if (zz)
+    k_brick3_single<T, true><<<grid, 64 * kBrickWaves, lds, st>>>(in, a, ebx2_r, r);
+  else
+    k_brick3_single<T, false><<<grid, 64 * kBrickWaves, lds, st>>>(in, a, ebx2_r, r);
+  if (hipError_t e = hipGetLastError()) return (int)e;
+  HeaderTpl t;
+  __builtin_memcpy(t.psz, psz_tpl, 176);
+  __builtin_memcpy(t.phf, phf_tpl, 64);
+  const uint32_t fgrid = std::max(1u, std::min((g.nbricks + 3) / 4, 1024u));
+  k_brick3_single_finish<<<fgrid, 256, 0, st>>>(a, t, s.archive, s.phf_offset, s.bits_rel, pub);
+  return (int)hipGetLastError();
+}
+
+template int launch_brick_sample<float>(const BrickLaunch&, const float*, double, int, bool, uint32_t*, int, hipStream_t);
+template int launch_brick_sample<double>(const BrickLaunch&, const double*, double, int, bool, uint32_t*, int, hipStream_t);
+template int launch_brick_single<float>(const BrickLaunch&, const float*, double, int, bool, const BrickSingle&,
+                                        const void*, const void*, hipStream_t, const HostPub&);
+template int launch_brick_single<double>(const BrickLaunch&, const double*, double, int, bool, const BrickSingle&,
+                                         const void*, const void*, hipStream_t, const HostPub&);
 
 int launch_brick_cell_bounds(const BrickLaunch& L, const uint32_t* cells, size_t ncell, uint32_t* bstart,
                              uint32_t* unsorted, uint32_t epoch, hipStream_t st)

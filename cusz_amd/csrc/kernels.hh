@@ -268,6 +268,29 @@ int launch_brick_plan(const BrickLaunch& L, const BrickPlanArgs& a, const void* 
 int launch_brick_pack(const BrickLaunch& L, const BrickCodes& bc, const uint32_t* book, int bklen,
                       const BrickPlanArgs& plan, uint32_t* par_nbit, uint32_t* par_entry, uint32_t* bitstream,
                       int reverse, unsigned int* overflow, hipStream_t st, const HostPub& pub = HostPub{});
+// sampled-codebook mode (3-D bricks): pass 0 = the histogram of every 16th brick; then one pass
+// predicts, sizes (decoupled look-back over the bricks) and packs each brick into the archive,
+// and a finish kernel writes the outlier segment, the totals and the headers
+template <typename T>
+int launch_brick_sample(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, uint32_t* hist, int bklen,
+                        hipStream_t st);
+struct BrickSingle {
+  OutlierSink ol;
+  BrickCodes bcs;  // c16: u16 rows; c0
+  const uint32_t* book;
+  int bklen;
+  uint32_t *par_nbit, *par_entry, *bitstream;
+  unsigned long long* status;  // nbricks words, zeroed per call
+  uint32_t* ticket;            // zeroed per call
+  uint32_t* ol_pre;            // nbricks
+  CompressInfo* info;          // zeroed per call
+  unsigned int* timeout;
+  uint8_t* archive;
+  size_t phf_offset, bits_rel;
+};
+template <typename T>
+int launch_brick_single(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const BrickSingle& s,
+                        const void* psz_tpl, const void* phf_tpl, hipStream_t st, const HostPub& pub);
 // Outlier cells for the fused decoder: when the archive's cells are grouped by brick and sorted
 // by (row, x) (k_brick_cell_bounds checks; this compressor writes them so), the decoder ranks the
 // zero codes of each row against the brick's cells and no scatter pass is needed; otherwise

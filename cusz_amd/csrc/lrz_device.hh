@@ -15,7 +15,12 @@ namespace lrzd {
 template <typename T>
 __device__ __forceinline__ T dround(T v);
 template <>
-__device__ __forceinline__ float dround<float>(float v) { return roundf(v); }
+__device__ __forceinline__ float dround<float>(float v)
+{
+  // roundf (half away from zero) as trunc(v + copysign(pred(0.5), v)): 3 VALU instead of 6;
+  // identical for every f32 (checked exhaustively on the host), including -0, ties and |v| >= 2^23
+  return __builtin_truncf(v + __builtin_copysignf(0.49999997f, v));
+}
 template <>
 __device__ __forceinline__ double dround<double>(double v) { return round(v); }
 

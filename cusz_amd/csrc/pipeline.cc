@@ -80,6 +80,7 @@ struct Pipeline {
   BrickLaunch bl{};               // fused brick path (brick.hip); bl.g.ok when eligible
   int layout = 0;                 // PSZ_AMD_LAYOUT_*: 0 brick layout when eligible, 1 reference layout
   bool layout_set = false;        // the caller chose the layout (psz_amd_set_layout)
+  int codebook = 0;               // PSZ_AMD_CODEBOOK_*: exact (full histogram) or sampled (one pass)
   uint16_t* d_bhist = nullptr;    // per-brick u16 histograms (pass 1 -> reservation)
   uint32_t* d_ub = nullptr;       // per-brick region upper bounds (cells)
   uint32_t* d_bbase = nullptr;    // per-brick cell offsets inside their plan block
@@ -328,6 +329,8 @@ struct Pipeline {
   template <typename T>
   int compress(psz_header* h, const T* in, uint8_t** out, size_t* outlen)
   {
+    if (codebook == PSZ_AMD_CODEBOOK_SAMPLED && bl.g.ndim == 3 && use_brick(h->pipeline.predictor))
+      return compress_sampled<T>(h, in, out, outlen);
     const int s = compress_scan<T>(h, in, true);
     return s ? s : compress_finish(h, nullptr, out, outlen);
   }
@@ -601,6 +604,84 @@ struct Pipeline {
     mark(4);
     if (gated)
       if (int fs = build_book()) return fs;
+    mark(5);
+    return finish_compress(h, out, outlen);
+  }
+
+  // Sampled-codebook mode (3-D bricks): the histogram of every 16th brick (+1 per bin) gives the
+  // codebook before the field is predicted; one pass then predicts and packs each brick at its
+  // look-back offset, and a finish kernel writes the outlier segment and the headers.  Codes,
+  // outliers and the reconstruction equal the exact mode's; the bitstream does not.
+  template <typename T>
+  int compress_sampled(psz_header* h, const T* in, uint8_t** out, size_t* outlen)
+  {
+    pend.active = false;
+    if (h->pipeline.codec1 != Huffman) return PSZ_ABORT_NO_SUCH_CODEC;
+    const bool zz = h->pipeline.predictor == LorenzoZigZag;
+    const int radius = h->rc.radius, bklen = 2 * radius;
+    if (radius < 1 || bklen > kMaxBklen) return PSZ_ABORT_NOT_IMPLEMENTED;
+    const BrickGeom& g = bl.g;
+    mark(0);
+    if (h->rc.mode == Rel) {  // libcusz.cc:287-293
+      CUSZ_AMD_HIP_CHECK((hipError_t)launch_extrema<T>(in, n, minmax(), ext_scratch(), stream));
+      int fs = fetch(regions({{h_readback() + 512, minmax(), 16}}), 1);
+      if (fs) return fs;
+      double mm[2];
+      std::memcpy(mm, h_readback() + 512, 16);
+      h->min_val = mm[0], h->max_val = mm[1];
+      h->rc.eb *= (mm[1] - mm[0]);
+    }
+    const double eb = h->rc.eb;
+    // look-back status words live in the per-brick histogram area (unused in this mode)
+    unsigned long long* status = reinterpret_cast<unsigned long long*>(d_bhist);
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_zero(regions({{d_hist, nullptr, (size_t)bklen * 4},
+                                                        {d_small, nullptr, 64 + sizeof(CompressInfo)},
+                                                        {status, nullptr, (size_t)g.nbricks * 8}}),
+                                               stream));
+    mark(1);
+    last_layout = PSZ_AMD_LAYOUT_BRICK;
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_sample<T>(bl, in, eb, radius, zz, d_hist, bklen, stream));
+    mark(2);
+    int fs = fetch(regions({{h_hist(), d_hist, (size_t)bklen * 4}}), 2);
+    if (fs) return fs;
+    for (int i = 0; i < bklen; i++) h_hist()[i] += 1;  // every code encodable
+    build_codebook(h_hist(), bklen, h_book(), h_revbook());
+    const size_t phf_off = 176;
+    const size_t rvbk = rvbk_bytes(bklen);
+    const int bsub = g.W, bpar = (int)g.nchunks;
+    const size_t nbit_rel = 128 + rvbk, entry_rel = nbit_rel + 4 * (size_t)bpar;
+    const size_t bits_rel = entry_rel + 4 * (size_t)bpar;
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_upload(
+        regions({{d_book, h_book(), (size_t)bklen * 4}, {d_archive + phf_off + 128, h_revbook(), rvbk}}), stream));
+    mark(3);
+    h->vle_sublen = bsub;
+    h->vle_pardeg = bpar;
+    h->len = len;
+    h->entry[0] = 0, h->entry[1] = 176, h->entry[2] = (uint32_t)phf_off;
+    phf_header ph;
+    std::memset(&ph, 0, sizeof(ph));
+    ph.bklen = bklen, ph.sublen = bsub, ph.pardeg = bpar, ph.original_len = n;
+    ph.entry[0] = 0, ph.entry[1] = 128, ph.entry[2] = (uint32_t)nbit_rel, ph.entry[3] = (uint32_t)entry_rel;
+    ph.entry[4] = (uint32_t)bits_rel;
+    BrickSingle sg{OutlierSink{d_slots, d_brick_cnt, d_spill, spill_cnt(), brick_cap(), spill_cap, nullptr},
+                   brick_codes(zz, radius),
+                   d_book,
+                   bklen,
+                   reinterpret_cast<uint32_t*>(d_archive + phf_off + nbit_rel),
+                   reinterpret_cast<uint32_t*>(d_archive + phf_off + entry_rel),
+                   reinterpret_cast<uint32_t*>(d_archive + phf_off + bits_rel),
+                   status,
+                   &info()->pad[1],
+                   d_ub,
+                   info(),
+                   timeout(),
+                   d_archive,
+                   phf_off,
+                   bits_rel};
+    const HostPub sp{readback_regions(), const_cast<uint32_t*>(flag(3)), ++epoch, reinterpret_cast<uint32_t*>(d_small + 20)};
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_single<T>(bl, in, eb, radius, zz, sg, h, &ph, stream, sp));
+    summary_epoch = sp.epoch;
+    mark(4);
     mark(5);
     return finish_compress(h, out, outlen);
   }
@@ -1091,6 +1172,14 @@ int psz_amd_set_decoder(psz_resource* m, int kind)
   Pipeline* p = cusz_amd::P(m);
   if (!p || kind < PSZ_AMD_DECODER_AUTO || kind > PSZ_AMD_DECODER_WAVE) return PSZ_ABORT_NOT_IMPLEMENTED;
   p->decoder = kind;
+  return PSZ_SUCCESS;
+}
+
+int psz_amd_set_codebook(psz_resource* m, int mode)
+{
+  Pipeline* p = cusz_amd::P(m);
+  if (!p || (mode != PSZ_AMD_CODEBOOK_EXACT && mode != PSZ_AMD_CODEBOOK_SAMPLED)) return PSZ_ABORT_NOT_IMPLEMENTED;
+  p->codebook = mode;
   return PSZ_SUCCESS;
 }
 

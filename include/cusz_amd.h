@@ -79,6 +79,17 @@ int psz_amd_set_decoder(psz_resource* m, int kind);
 #define PSZ_AMD_LAYOUT_REFERENCE 1
 int psz_amd_set_layout(psz_resource* m, int layout);
 
+/* Codebook source (brick layout, 3-D fields; other fields always use EXACT).
+ *  EXACT (default): the codebook of the full histogram, as the reference (compressor.inl:339-458):
+ *    pass 1 predicts and counts, pass 2 packs.
+ *  SAMPLED: the codebook of the histogram of every 16th brick, +1 on every bin, built before the
+ *    field is predicted; one pass then predicts and packs.  Quant codes, outliers, the error bound
+ *    and the decompressed field are identical to EXACT; the bitstream (and CR) differ.  The
+ *    archive is an ordinary phf archive: the reference decoder reads it. */
+#define PSZ_AMD_CODEBOOK_EXACT 0
+#define PSZ_AMD_CODEBOOK_SAMPLED 1
+int psz_amd_set_codebook(psz_resource* m, int mode);
+
 /* ---- sharded compress (multi-GPU; the reference has no multi-GPU path) ----
  * A field split into tile-aligned slabs (z: multiples of 8 planes) is compressed one slab per
  * GPU with ONE codebook:

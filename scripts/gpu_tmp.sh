@@ -1,7 +1,6 @@
 #!/bin/bash
+# scratch GPU check: sampled-codebook mode tests, then the brick suite, then a timing line
 export TMPDIR=/tmp
-scripts/gpu_job.sh "tests:600:python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider" || exit 1
-echo "== lib" >> gpurun_out/var.log
-timeout -k 10 60 python scripts/brick_bench.py --reps 20 >> gpurun_out/var.log 2>&1 || exit 1
-timeout -k 10 60 python scripts/brick_bench.py --dims 280953867x1x1 --reps 10 >> gpurun_out/var.log 2>&1 || exit 1
-timeout -k 10 120 rocprofv3 --kernel-trace -d gpurun_out/kt -o kt --output-format csv -- python3 scripts/brick_bench.py --reps 3 > gpurun_out/kt.log 2>&1
+exec scripts/gpu_job.sh \
+  "sampled:200:python -u -m pytest tests/test_gpu_sampled.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider" \
+  "tests:400:python -u -m pytest tests -x -q -m gpu --timeout 200 --timeout-method thread -p no:cacheprovider"
