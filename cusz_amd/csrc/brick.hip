@@ -1872,6 +1872,9 @@ struct SingleArgs {
 };
 
 constexpr int kSingleWaveWords = 64 * 64 + pack_cells_words<4>();  // byte rows + packing cells
+#ifndef CUSZ_AMD_SINGLE_AHEAD
+#define CUSZ_AMD_SINGLE_AHEAD 16
+#endif
 
 template <typename T, bool ZZ>
 __global__ void __launch_bounds__(64 * kBrickWaves)
@@ -1894,7 +1897,8 @@ k_brick3_single(const T* __restrict__ in, SingleArgs a, T ebx2_r, T r)
     if (lane == 0) b = atomicAdd(a.ticket, 1u);
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
   };
-  constexpr int D = kScanAhead<T>;
+  // rows in flight per wave: two y-steps (f32), as LDS allows only 8 waves per CU here
+  constexpr int D = sizeof(T) == 4 ? CUSZ_AMD_SINGLE_AHEAD : 8;
   uint32_t brick = claim();
   T q[D][V];
 #pragma unroll

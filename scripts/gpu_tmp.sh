@@ -1,6 +1,6 @@
 #!/bin/bash
-# scratch GPU check: config-2 bench with the sampled-codebook leg, kernel stats
+# scratch GPU check: sampled-codebook parity, micro-bench
 export TMPDIR=/tmp
 exec scripts/gpu_job.sh \
-  "bench:300:python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-e2e" \
-  "stats:300:rocprofv3 --kernel-trace --stats -d gpurun_out/prof_stats -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-e2e --profile-only"
+  "sampled:200:python -u -m pytest tests/test_gpu_sampled.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider" \
+  "single:60:python scripts/single_bench.py"
