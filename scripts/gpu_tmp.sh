@@ -1,6 +1,10 @@
 #!/bin/bash
-# scratch GPU check: sampled-codebook parity, micro-bench
+# round-end measurement: GPU suite, smoke, config-2 bench (CPU baseline, e2e), config-2 profile
+# (stats + FETCH/WRITE), config-3 bench
 export TMPDIR=/tmp
 exec scripts/gpu_job.sh \
-  "sampled:200:python -u -m pytest tests/test_gpu_sampled.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider" \
-  "single:60:python scripts/single_bench.py"
+  "tests:400:python -u -m pytest tests -x -q -m gpu --timeout 200 --timeout-method thread -p no:cacheprovider" \
+  "smoke:120:python -c 'import __graft_entry__ as g; g.smoke()'" \
+  "bench:300:python bench.py --steps 20 --warmup 5" \
+  "prof2:500:bash scripts/pmc_config.sh r03_c2 2" \
+  "bench3:300:python bench.py --config 3 --steps 10 --warmup 3"
