@@ -9,9 +9,10 @@
 // MI355X layout.  A wave owns a brick of W x 8 x 8 elements (W = 64 V: lane l holds x in
 // [l V, l V + V)).  The Huffman chunk length is W, so every brick ROW (fixed y, z) is exactly one
 // reference chunk: chunk c covers codes [c W, c W + W) of the linear (x-fastest) order.
-//   pass 1 (k_brick3_scan):  predict -> codes in brick order (u16), per-unit histogram (u16,
-//                            kept for the plan), global histogram, outlier slots.  Reads the
-//                            input once.
+//   pass 1 (k_brick3_scan):  predict -> codes in brick order (byte rows; u16 rows when a code
+//                            leaves the byte window, one mask bit per row), per-unit histogram
+//                            (u16, kept for the plan), global histogram, outlier slots.  Reads
+//                            the input once.
 //   host:                    canonical codebook from the global histogram (exact reference heap).
 //   plan (k_brick_plan):     a unit's bits = sum(hist_u[s] * len[s]); its region in the bitstream
 //                            is that many bits plus one partial cell per row -- an upper bound,
@@ -23,6 +24,9 @@
 //   decompress (k_brick3_decode): one wave per brick, one chunk per lane decoded in x-blocks of
 //                            64 symbols into an LDS code tile; the block is reconstructed
 //                            (reference scan order) and stored as whole rows.
+// Sampled-codebook mode (k_brick3_sample, k_brick3_single, k_brick3_single_finish): the book
+// comes from every 16th brick before the field is predicted, and one pass predicts, sizes (look-
+// back over the bricks) and packs each brick; see the section before the launchers.
 // The archive is the reference phf format: par_entry[c] points at chunk c (the reference decoder
 // reads chunk c from there, hf_kernels.cuhip.inl:386-391); chunks are laid out brick by brick,
 // and the few cells between a brick's last chunk and the next region are zero.
