@@ -197,16 +197,27 @@ __global__ void __launch_bounds__(64 * kPackWaves) k_hf_pack(HfEncodeArgs a, int
 // per-tile cell totals (tile = kGatherTile consecutive chunks), one wave per tile
 constexpr int kGatherTile = 64;
 
+// (and, when total_nbit is set, the archive's bit total: one 64-bit atomic per tile, so the
+// finalize step needs no summing launch of its own)
 __global__ void __launch_bounds__(256) k_hf_tile_sums(const uint32_t* __restrict__ par_nbit, int pardeg,
-                                                      uint32_t* __restrict__ tile_sum, int ntiles)
+                                                      uint32_t* __restrict__ tile_sum, int ntiles,
+                                                      unsigned long long* total_nbit)
 {
   const int lane = threadIdx.x & 63;
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= ntiles) return;
-  uint32_t acc = 0;
-  for (int i = t * kGatherTile + lane; i < min((t + 1) * kGatherTile, pardeg); i += 64) acc += (par_nbit[i] + 31) >> 5;
+  uint32_t acc = 0, bits = 0;
+  for (int i = t * kGatherTile + lane; i < min((t + 1) * kGatherTile, pardeg); i += 64) {
+    const uint32_t nb = par_nbit[i];
+    acc += (nb + 31) >> 5;
+    bits += nb;  // a tile of 64 chunks of <= 8192 codes of <= 27 bits: < 2^32
+  }
   acc = wave_sum(acc);
-  if (lane == 0) tile_sum[t] = acc;
+  bits = wave_sum(bits);
+  if (lane == 0) {
+    tile_sum[t] = acc;
+    if (total_nbit) atomicAdd(total_nbit, (unsigned long long)bits);
+  }
 }
 
 // exclusive scan of the tile totals in place (one workgroup; ntiles <= 1024 * 8)
@@ -892,7 +903,7 @@ int launch_hf_encode(const HfEncodeArgs& a, hipStream_t st)
   k_hf_pack<<<grid, 64 * kPackWaves, lds, st>>>(a, cellcap);
   const int ntiles = (a.pardeg + kGatherTile - 1) / kGatherTile;
   uint32_t* tile_sum = a.temp + hf_encode_temp_words(a.sublen, a.pardeg) - hf_encode_tile_words(a.pardeg);
-  k_hf_tile_sums<<<(ntiles + 3) / 4, 256, 0, st>>>(a.par_nbit, a.pardeg, tile_sum, ntiles);
+  k_hf_tile_sums<<<(ntiles + 3) / 4, 256, 0, st>>>(a.par_nbit, a.pardeg, tile_sum, ntiles, a.total_nbit);
   k_hf_tile_scan<<<1, 1024, 0, st>>>(tile_sum, ntiles);
   k_hf_gather<<<ntiles, 256, 0, st>>>(a, cellcap, tile_sum);
   return (int)hipGetLastError();

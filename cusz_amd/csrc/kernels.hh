@@ -59,6 +59,7 @@ struct HfEncodeArgs {
   unsigned long long* status;  // pardeg/kGroup+1 lookback words, zeroed before launch
   unsigned int* timeout;       // set nonzero if a bounded spin gave up
   uint32_t* temp;              // scratch of hf_encode_temp_words(); nullptr = look-back encoder
+  unsigned long long* total_nbit = nullptr;  // if set (zeroed before): the tile-sum pass adds every chunk's bits
 };
 int launch_hf_encode(const HfEncodeArgs& a, hipStream_t st);
 size_t hf_encode_temp_words(int sublen, int pardeg);
@@ -100,8 +101,12 @@ struct FinalizeArgs {
   CompressInfo* info;
   const uint32_t* spill_start = nullptr;  // OutlierSink::spill_start (ranged spill) or nullptr
   bool sizes_known = false;  // brick path: total_nbit / total_ncell already in info (reservation)
+  bool nbit_known = false;   // info->total_nbit already summed (the encoder's tile-sum pass)
 };
-int launch_finalize_scan(const FinalizeArgs& a, hipStream_t st);
+// psz_tpl / phf_tpl non-null: the same workgroup also writes both headers (no separate launch)
+int launch_finalize_scan(const FinalizeArgs& a, hipStream_t st, const void* psz_tpl = nullptr,
+                         const void* phf_tpl = nullptr, uint8_t* archive = nullptr, size_t phf_offset = 0,
+                         size_t bitstream_rel = 0);
 
 struct OutlierCopyArgs {
   const uint64_t* slots;
@@ -119,10 +124,6 @@ struct OutlierCopyArgs {
 };
 int launch_outlier_copy(const OutlierCopyArgs& a, hipStream_t st);
 
-// writes the psz_header (176 B) and phf_header (64 B + pad) with the dynamic fields filled
-int launch_write_headers(uint8_t* archive, const void* psz_hdr_tpl, const void* phf_hdr_tpl,
-                         const CompressInfo* info, size_t phf_offset, size_t bitstream_rel,
-                         hipStream_t st);
 
 // small host<->device transfers through host-mapped pinned memory (no stream sync)
 struct XferRegions {

@@ -490,17 +490,12 @@ struct Pipeline {
                     d_status,
                     timeout(),
                     d_enc_temp};
+    ea.total_nbit = &info()->total_nbit;  // summed by the encoder's tile-sum pass
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_hf_encode(ea, stream));
     mark(4);
 
-    FinalizeArgs fa{ea.par_nbit, ea.par_entry, pardeg, bcnt, nbr, cap, spill_cnt(), spill_cap, boff, info(),
-                    spill_start};
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_finalize_scan(fa, stream));
-    OutlierCopyArgs oa{slots, bcnt,      boff,           nbr, cap, d_spill, spill_cnt(), spill_cap,
-                       info(), d_archive, phf_off + bits_rel, spill_start};
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_outlier_copy(oa, stream));
-
-    // header templates: static fields from the host, dynamic ones filled on the device
+    // header templates: static fields from the host, dynamic ones filled on the device (by the
+    // finalize workgroup, which knows the totals)
     h->vle_sublen = sublen;
     h->vle_pardeg = pardeg;
     h->len = len;
@@ -510,8 +505,13 @@ struct Pipeline {
     ph.bklen = bklen, ph.sublen = sublen, ph.pardeg = pardeg, ph.original_len = n;
     ph.entry[0] = 0, ph.entry[1] = 128, ph.entry[2] = (uint32_t)nbit_rel, ph.entry[3] = (uint32_t)entry_rel;
     ph.entry[4] = (uint32_t)bits_rel;
-    CUSZ_AMD_HIP_CHECK(
-        (hipError_t)launch_write_headers(d_archive, h, &ph, info(), phf_off, bits_rel, stream));
+    FinalizeArgs fa{ea.par_nbit, ea.par_entry, pardeg, bcnt, nbr, cap, spill_cnt(), spill_cap, boff, info(),
+                    spill_start};
+    fa.nbit_known = true;
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_finalize_scan(fa, stream, h, &ph, d_archive, phf_off, bits_rel));
+    OutlierCopyArgs oa{slots, bcnt,      boff,           nbr, cap, d_spill, spill_cnt(), spill_cap,
+                       info(), d_archive, phf_off + bits_rel, spill_start};
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_outlier_copy(oa, stream));
     mark(5);
     return finish_compress(h, out, outlen);
   }

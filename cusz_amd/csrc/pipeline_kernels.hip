@@ -38,7 +38,8 @@ __global__ void __launch_bounds__(256) k_sum_nbit(const uint32_t* __restrict__ p
 // sums it with coalesced 16-byte loads, one barrier exchanges the segment sums, pass 2 scans
 // it 256 counts (4 per lane) at a time with a carry, the next group's load issued before the
 // current group's scan (65,536 spline tiles: the former 8-k-per-pass block scan took 63 us).
-__global__ void __launch_bounds__(1024) k_finalize_scan(FinalizeArgs a)
+__global__ void __launch_bounds__(1024) k_finalize_scan(FinalizeArgs a, HeaderTpl hdr, uint8_t* archive,
+                                                       size_t phf_offset, size_t bitstream_rel, int write_hdr)
 {
   __shared__ uint32_t s_scan[16];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -107,6 +108,8 @@ __global__ void __launch_bounds__(1024) k_finalize_scan(FinalizeArgs a)
     a.info->total_ncell = ncell;
     a.info->splen = (unsigned long long)slot_total + (a.spill_start ? 0u : sp_kept);
     a.info->outlier_lost = sp > a.spill_cap ? sp - a.spill_cap : 0u;
+    if (write_hdr)
+      write_headers_dev(archive, hdr, a.info->total_nbit, ncell, a.info->splen, phf_offset, bitstream_rel);
   }
 }
 
@@ -154,13 +157,6 @@ __global__ void __launch_bounds__(256) k_outlier_copy(OutlierCopyArgs a, uint32_
       d[2 * i + 1] = (uint32_t)(c >> 32);
     }
   }
-}
-
-__global__ void k_write_headers(uint8_t* archive, HeaderTpl t, const CompressInfo* info, size_t phf_offset,
-                                size_t bitstream_rel)
-{
-  if (threadIdx.x == 0)
-    write_headers_dev(archive, t, info->total_nbit, info->total_ncell, info->splen, phf_offset, bitstream_rel);
 }
 
 template <typename T>
@@ -320,12 +316,21 @@ int launch_upload(const XferRegions& r, hipStream_t st)
   return (int)hipGetLastError();
 }
 
-int launch_finalize_scan(const FinalizeArgs& a, hipStream_t st)
+int launch_finalize_scan(const FinalizeArgs& a, hipStream_t st, const void* psz_tpl, const void* phf_tpl,
+                         uint8_t* archive, size_t phf_offset, size_t bitstream_rel)
 {
   int grid = (a.pardeg + 255) / 256;
   grid = grid < 1 ? 1 : (grid > 128 ? 128 : grid);
-  if (!a.sizes_known) k_sum_nbit<<<grid, 256, 0, st>>>(a.par_nbit, a.pardeg, &a.info->total_nbit);
-  k_finalize_scan<<<1, 1024, 0, st>>>(a);
+  if (!a.sizes_known && !a.nbit_known) k_sum_nbit<<<grid, 256, 0, st>>>(a.par_nbit, a.pardeg, &a.info->total_nbit);
+  HeaderTpl t;
+  const int wh = psz_tpl && phf_tpl && archive;
+  if (wh) {
+    __builtin_memcpy(t.psz, psz_tpl, 176);
+    __builtin_memcpy(t.phf, phf_tpl, 64);
+  }
+  else
+    __builtin_memset(&t, 0, sizeof(t));
+  k_finalize_scan<<<1, 1024, 0, st>>>(a, t, archive, phf_offset, bitstream_rel, wh);
   return (int)hipGetLastError();
 }
 
@@ -334,16 +339,6 @@ int launch_outlier_copy(const OutlierCopyArgs& a, hipStream_t st)
   const uint32_t brick_blocks = (a.nbricks + 3) / 4;
   const uint32_t spill_blocks = 64;
   k_outlier_copy<<<brick_blocks + spill_blocks, 256, 0, st>>>(a, spill_blocks);
-  return (int)hipGetLastError();
-}
-
-int launch_write_headers(uint8_t* archive, const void* psz_hdr_tpl, const void* phf_hdr_tpl,
-                         const CompressInfo* info, size_t phf_offset, size_t bitstream_rel, hipStream_t st)
-{
-  HeaderTpl t;
-  __builtin_memcpy(t.psz, psz_hdr_tpl, 176);
-  __builtin_memcpy(t.phf, phf_hdr_tpl, 64);
-  k_write_headers<<<1, 64, 0, st>>>(archive, t, info, phf_offset, bitstream_rel);
   return (int)hipGetLastError();
 }
 
