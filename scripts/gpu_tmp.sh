@@ -1,7 +1,6 @@
 #!/bin/bash
-# GPU suite + config 1 / 5 benches after folding the finalize launches
+# round-end benches for configs 1 and 5 (config 2/3 lines are in profiles/ already)
 export TMPDIR=/tmp
 exec scripts/gpu_job.sh \
-  "tests:400:python -u -m pytest tests -x -q -m gpu --timeout 200 --timeout-method thread -p no:cacheprovider" \
-  "bench1:200:python bench.py --config 1 --steps 20 --warmup 3 --no-e2e" \
-  "bench5:300:python bench.py --config 5 --steps 10 --warmup 3 --no-e2e"
+  "bench1:200:python bench.py --config 1 --steps 20 --warmup 3" \
+  "bench5:300:python bench.py --config 5 --steps 10 --warmup 3"
