@@ -856,9 +856,10 @@ k_brick3_pack(BrickCodes bcs, uint32_t ly, uint32_t lz, const uint32_t* __restri
 // so the lane stands still, and one extra step after the quarter decodes it by threshold counting
 // (hf_device.hh lookup_long) for the lanes that need it.  A lane may thus run up to 2 kF + 1
 // symbols past the block end, into tile columns [64, 74), which move to the block's front after
-// the reconstruction.  Tile stores are aligned 32-bit pairs (a 2-B aligned 32-bit LDS store
-// stalls the LDS pipeline, SQ_LDS_UNALIGNED_STALL): at an even column the entry's two symbols,
-// at an odd column the symbol kept from the previous step and this step's first.
+// the reconstruction.  Tile stores: each step writes both symbol slots of its entry as two
+// naturally aligned u16 stores (ds_write_b16 / _d16_hi of one register; a compiler barrier keeps
+// them from merging into a 2-B aligned b32 store, which stalls the LDS pipeline); a slot past
+// the entry's symbols is overwritten by the next step.
 //
 // Outliers.  When the archive's cells are grouped by brick and sorted by (row, x) -- this
 // compressor writes them so, k_brick_cell_bounds checks -- the k-th zero code of a row takes the
@@ -1198,7 +1199,6 @@ __device__ __forceinline__ void decode_chunks(const hfd::LdsTables<kDecB>& tb, c
   uint32_t ltop = 8;  // words [0, ltop) have been requested
   uint32_t sh = 0;    // 32 - bits of w0 consumed
   uint32_t cnt = live ? 0u : 0x40000000u;  // symbols decoded; a dead lane never steps
-  uint32_t keep = 0;  // symbol at the even column before an odd cnt (see the tile stores)
   uint32_t rdy = ctop >= nwords ? 0xFFFFFFFFu : ctop;  // words [0, rdy) are readable
   u32x4 pa, pb;       // groups in flight
   bool fa = false, fb = false;
@@ -1235,10 +1235,12 @@ __device__ __forceinline__ void decode_chunks(const hfd::LdsTables<kDecB>& tb, c
           // a code longer than 16 bits has no table entry: e = 0 consumes nothing, and the lane
           // decodes it after the quarter (rare: no branch in the steps)
           e = lng ? hfd::lookup_long<kDecB>(tb, rg, win, dw.ubk) : hfd::lookup_short<kDecB>(tb, rg, win);
+          // both symbol slots written as naturally aligned u16 stores (the low and high halves
+          // of one register); a slot past the entry's symbols is overwritten by the next step
           const uint32_t sy = e & hfd::kEntSymMask;
-          const bool odd = cnt & 1u;
-          *reinterpret_cast<uint32_t*>(rowp + (cnt & ~1u)) = odd ? (keep | (sy << 16)) : sy;
-          keep = e == 0 ? keep : (odd ? (sy >> 16) : (sy & 0xFFFFu));
+          rowp[cnt] = (uint16_t)sy;
+          asm volatile("" ::: "memory");  // two u16 stores: merged they would be an unaligned b32
+          rowp[cnt + 1] = (uint16_t)(sy >> 16);
           cnt += hfd::ent_nsym(e);
           const int32_t s2 = (int32_t)sh - (int32_t)hfd::ent_bits(e);
           const bool shf = s2 < 0;  // crossed into the next word
@@ -1276,7 +1278,7 @@ __device__ __forceinline__ void decode_chunks(const hfd::LdsTables<kDecB>& tb, c
     consume(pb, fb);
     hfd::wave_sync();
     BPROF(tk = __builtin_readcyclecounter(); pc[3] += tk - tp; tp = tk;)
-    // symbols decoded past the block end move to its front (`keep` carries a pending one); they
+    // symbols decoded past the block end move to its front; they
     // are held in registers across the reconstruction, which may use the tile as scratch
     uint32_t* rw = reinterpret_cast<uint32_t*>(dw.tile + lane * kTP);
     uint32_t ovs[kF + 1];
