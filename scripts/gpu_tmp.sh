@@ -1,7 +1,9 @@
 #!/bin/bash
-# decoder tile-store change: full GPU suite, config-2 and config-3 benches
+# round-end measurement after the decoder change: smoke, config-2 bench + profile, config-3 bench
 export TMPDIR=/tmp
 exec scripts/gpu_job.sh \
-  "tests:400:python -u -m pytest tests -x -q -m gpu --timeout 200 --timeout-method thread -p no:cacheprovider" \
-  "bench:300:python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-e2e" \
-  "bench3:300:python bench.py --config 3 --steps 10 --warmup 3 --no-cpu-baseline --no-e2e"
+  "smoke:120:python -c 'import __graft_entry__ as g; g.smoke()'" \
+  "bench:300:python bench.py --steps 20 --warmup 5" \
+  "prof2:500:bash scripts/pmc_config.sh r03_c2 2" \
+  "bench3:300:python bench.py --config 3 --steps 10 --warmup 3" \
+  "prof3:500:bash scripts/pmc_config.sh r03_c3 3"
