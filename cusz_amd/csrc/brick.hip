@@ -117,6 +117,10 @@ __device__ __forceinline__ void residual_ystep(uint32_t x0, int y, T (&bprev)[8]
 // NB = 2 for f32 (16 KiB in flight per wave at 2 waves/SIMD); f64 rows are twice as wide: 1.
 template <typename T>
 constexpr int kStepBuffers = sizeof(T) == 4 ? 2 : 1;
+#ifndef CUSZ_AMD_SCAN_LOAD_AUX
+#define CUSZ_AMD_SCAN_LOAD_AUX 2  // cache-policy bits of pass 1's field loads: 2 = nontemporal
+// (config 2 pass 1 189 -> 163 us: the streamed field no longer evicts the code rows pass 2 reads)
+#endif
 template <typename T, int V>
 struct StepLoader {
   const T* in;
@@ -143,7 +147,7 @@ struct StepLoader {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int h = 0; h < (int)(V * sizeof(T) / 16); h++) {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + 16 * h), 0, 0);
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + 16 * h), 0, CUSZ_AMD_SCAN_LOAD_AUX);
       __builtin_memcpy(reinterpret_cast<char*>(&dst[0]) + 16 * h, &v, 16);
     }
   }
@@ -164,7 +168,7 @@ struct StepLoader {
       typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
       for (int h = 0; h < (int)(V * sizeof(T) / 16); h++) {
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + 16 * h), 0, 0);
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + 16 * h), 0, CUSZ_AMD_SCAN_LOAD_AUX);
         __builtin_memcpy(reinterpret_cast<char*>(&dst[z][0]) + 16 * h, &v, 16);
       }
     }
@@ -451,7 +455,7 @@ k_brick1_scan(const T* __restrict__ in, size_t n, T ebx2_r, T r, OutlierSink ol,
     const uint32_t off = ((uint32_t)row * (64 * V) + x0) * (uint32_t)sizeof(T);
 #pragma unroll
     for (int h = 0; h < (int)(V * sizeof(T) / 16); h++) {
-      const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + 16 * h), 0, 0);
+      const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + 16 * h), 0, CUSZ_AMD_SCAN_LOAD_AUX);
       __builtin_memcpy(reinterpret_cast<char*>(&dst[0]) + 16 * h, &v, 16);
     }
   };
