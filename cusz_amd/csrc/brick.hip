@@ -945,18 +945,22 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const T* base)
 {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(base), 0, (int)0xFFFFFFFF, (int)kBufRsrcW3);
 }
+#ifndef CUSZ_AMD_OUT_STORE_AUX
+#define CUSZ_AMD_OUT_STORE_AUX 2  // cache-policy bits of the decoders' output stores: 2 = nontemporal
+// (config 2 858 -> 893 GB/s: the written field no longer evicts what the next step reads)
+#endif
 template <typename T>
 __device__ __forceinline__ void buf_store(T v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff);
 template <>
 __device__ __forceinline__ void buf_store<float>(float v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff)
 {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)voff, (int)soff, 0);
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)voff, (int)soff, CUSZ_AMD_OUT_STORE_AUX);
 }
 template <>
 __device__ __forceinline__ void buf_store<double>(double v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff)
 {
   typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, (int)voff, (int)soff, 0);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, (int)voff, (int)soff, CUSZ_AMD_OUT_STORE_AUX);
 }
 
 // four consecutive elements (16 B for f32, 32 B for f64) at byte offset voff
@@ -967,7 +971,7 @@ __device__ __forceinline__ void buf_store4(const T* v, __amdgpu_buffer_rsrc_t r,
   u32x4v w[sizeof(T) / 4];
   __builtin_memcpy(&w[0], v, 4 * sizeof(T));
 #pragma unroll
-  for (int i = 0; i < (int)sizeof(T) / 4; i++) __builtin_amdgcn_raw_buffer_store_b128(w[i], r, (int)(voff + 16 * i), 0, 0);
+  for (int i = 0; i < (int)sizeof(T) / 4; i++) __builtin_amdgcn_raw_buffer_store_b128(w[i], r, (int)(voff + 16 * i), 0, CUSZ_AMD_OUT_STORE_AUX);
 }
 
 template <typename T>
