@@ -27,12 +27,20 @@ HistogramGeneric, HistogramSparse = 0, 1
 PSZ_SUCCESS = 0
 PSZ_WARN_RADIUS_TOO_LARGE = 1
 PSZ_WARN_OUTLIER_TOO_MANY = 2
+PSZ_ABORT_UNSUPPORTED_TYPE = 3
+PSZ_ABORT_UNSUPPORTED_DIMENSION = 4
 STATUS_NAMES = [
     "PSZ_SUCCESS", "PSZ_WARN_RADIUS_TOO_LARGE", "PSZ_WARN_OUTLIER_TOO_MANY",
     "PSZ_ABORT_UNSUPPORTED_TYPE", "PSZ_ABORT_UNSUPPORTED_DIMENSION", "PSZ_ABORT_NOT_IMPLEMENTED",
     "PSZ_ABORT_NO_SUCH_PREDICTOR", "PSZ_ABORT_NO_SUCH_CODEC", "PSZ_ABORT_TOO_MANY_UNPREDICTABLE",
     "PSZ_ABORT_TOO_MANY_ENC_BREAK",
 ]
+
+# extensions beyond psz_error_status (include/cusz_amd.h)
+PSZ_AMD_ERR_INVALID_ARG, PSZ_AMD_ERR_BAD_ARCHIVE, PSZ_AMD_ERR_DEVICE, PSZ_AMD_ERR_STATE, PSZ_AMD_ERR_ENCODER = (
+    100, 101, 102, 103, 104)
+EXT_STATUS_NAMES = {100: "PSZ_AMD_ERR_INVALID_ARG", 101: "PSZ_AMD_ERR_BAD_ARCHIVE", 102: "PSZ_AMD_ERR_DEVICE",
+                    103: "PSZ_AMD_ERR_STATE", 104: "PSZ_AMD_ERR_ENCODER"}
 
 T_EXTREMA, T_PREDICT, T_BOOK, T_ENCODE, T_FINALIZE, T_COMPRESS = range(6)
 T_SCATTER, T_DECODE, T_RECON, T_DECOMPRESS, T_COUNT = 6, 7, 8, 9, 10
@@ -167,13 +175,13 @@ def lib():
 # Huffman decoder selection (include/cusz_amd.h PSZ_AMD_DECODER_*)
 DECODER_AUTO, DECODER_LANE, DECODER_WAVE = 0, 1, 2
 # archive layout (PSZ_AMD_LAYOUT_*)
-LAYOUT_BRICK, LAYOUT_REFERENCE = 0, 1
+LAYOUT_BRICK, LAYOUT_REFERENCE, LAYOUT_BRICK_FORCE = 0, 1, 2
 CODEBOOK_EXACT, CODEBOOK_SAMPLED = 0, 1
 
 
 class PszError(RuntimeError):
     def __init__(self, status: int, what: str):
-        name = STATUS_NAMES[status] if 0 <= status < len(STATUS_NAMES) else str(status)
+        name = STATUS_NAMES[status] if 0 <= status < len(STATUS_NAMES) else EXT_STATUS_NAMES.get(status, str(status))
         super().__init__(f"{what} failed: {name}")
         self.status = status
 
@@ -191,8 +199,9 @@ class Resource:
                 dtype, psz_len(x, y, z), psz_pipeline(predictor, HistogramGeneric, Huffman, NullCodec),
                 C.c_void_p(stream))
         if not self._h:
-            raise PszError(5, "psz_create_resource_manager")
+            raise PszError(PSZ_AMD_ERR_DEVICE, "psz_create_resource_manager")
         self.dtype = dtype if header is None else header.dtype
+        self.stream = int(stream or 0)  # the manager's HIP stream handle (0: the null stream)
         self.header = psz_header()
 
     def close(self):
@@ -274,7 +283,8 @@ class Resource:
             raise PszError(st, "psz_amd_set_decoder")
 
     def set_layout(self, layout: int):
-        """LAYOUT_BRICK (fused, default when eligible) or LAYOUT_REFERENCE (byte-identical)."""
+        """LAYOUT_BRICK (fused, default when eligible), LAYOUT_REFERENCE (byte-identical) or
+        LAYOUT_BRICK_FORCE (bricks also for 2-D fields too small for them to pay)."""
         st = lib().psz_amd_set_layout(self._h, int(layout))
         if st != PSZ_SUCCESS:
             raise PszError(st, "psz_amd_set_layout")
@@ -316,9 +326,9 @@ def merge_archives(parts, full_dims, offsets=None) -> bytes:
     offs = (C.c_size_t * len(parts))(*offsets) if offsets is not None else None
     x, y, z = (tuple(full_dims) + (1, 1, 1))[:3]
     need = C.c_size_t()
-    L.psz_amd_merge_archives(ptrs, sizes, len(parts), offs, psz_len(x, y, z), None, 0, C.byref(need))
-    if need.value == 0:
-        raise PszError(5, "psz_amd_merge_archives")
+    st = L.psz_amd_merge_archives(ptrs, sizes, len(parts), offs, psz_len(x, y, z), None, 0, C.byref(need))
+    if st != PSZ_SUCCESS:
+        raise PszError(st, "psz_amd_merge_archives")
     out = C.create_string_buffer(need.value)
     st = L.psz_amd_merge_archives(ptrs, sizes, len(parts), offs, psz_len(x, y, z), out, need.value,
                                   C.byref(need))

@@ -136,7 +136,7 @@ void pszctx_create_from_argv(psz_ctx* ctx, int const argc, char** const argv)
   auto need = [&](int i) -> bool {
     if (i + 1 >= argc) {
       std::fprintf(stderr, "[cusz] missing value after %s\n", argv[i]);
-      ctx->last_error = PSZ_ABORT_NOT_IMPLEMENTED;
+      ctx->last_error = (psz_error_status)PSZ_AMD_ERR_INVALID_ARG;
       return false;
     }
     return true;
@@ -251,7 +251,7 @@ void pszctx_create_from_argv(psz_ctx* ctx, int const argc, char** const argv)
     }
     else {
       std::fprintf(stderr, "[cusz] invalid option at position %d: %s\n", i, a);
-      ctx->last_error = PSZ_ABORT_NOT_IMPLEMENTED;
+      ctx->last_error = (psz_error_status)PSZ_AMD_ERR_INVALID_ARG;
       return;
     }
   }
@@ -307,7 +307,7 @@ static psz_compressor* wrap(psz_ctx* ctx)
   comp->mem = nullptr;
   comp->compressor = nullptr;
   if (!ctx) {
-    comp->last_error = PSZ_ABORT_NOT_IMPLEMENTED;
+    comp->last_error = (psz_error_status)PSZ_AMD_ERR_INVALID_ARG;
     return comp;
   }
   if (ctx->header->dtype != F4 && ctx->header->dtype != F8) {
@@ -316,7 +316,7 @@ static psz_compressor* wrap(psz_ctx* ctx)
   }
   phf_coarse_tune(ctx->len_linear, &ctx->header->vle_sublen, &ctx->header->vle_pardeg);
   psz_resource* m = psz_create_resource_manager_from_header(ctx->header, nullptr);
-  if (!m) comp->last_error = PSZ_ABORT_NOT_IMPLEMENTED;
+  if (!m) comp->last_error = (psz_error_status)PSZ_AMD_ERR_DEVICE;  // allocation or runtime failure
   comp->compressor = m;
   return comp;
 }
@@ -372,7 +372,7 @@ pszerror psz_compress(psz_compressor* comp, void* d_in, psz_len3 const in_len3, 
                       void* record, void* stream)
 {
   (void)record;
-  if (!comp || !comp->compressor) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if (!comp || !comp->compressor) return (pszerror)PSZ_AMD_ERR_INVALID_ARG;
   auto* m = (psz_resource*)comp->compressor;
   if (in_len3.x != m->header->len.x || in_len3.y != m->header->len.y || in_len3.z != m->header->len.z)
     return PSZ_ABORT_UNSUPPORTED_DIMENSION;
@@ -391,7 +391,7 @@ pszerror psz_decompress(psz_compressor* comp, uint8_t* d_compressed, size_t cons
 {
   (void)record;
   (void)decomp_len;
-  if (!comp || !comp->compressor) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if (!comp || !comp->compressor) return (pszerror)PSZ_AMD_ERR_INVALID_ARG;
   auto* m = (psz_resource*)comp->compressor;
   cusz_amd_set_stream(m, stream);
   psz_modify_resource_manager_from_header(m, comp->ctx->header);

@@ -878,6 +878,9 @@ k_brick3_pack(BrickCodes bcs, uint32_t ly, uint32_t lz, const uint32_t* __restri
 #ifndef CUSZ_AMD_DEC_WAVES
 #define CUSZ_AMD_DEC_WAVES 8
 #endif
+#ifndef CUSZ_AMD_DEC_G
+#define CUSZ_AMD_DEC_G 2  // ring refill groups in flight (2 or 4)
+#endif
 constexpr int kDecB = CUSZ_AMD_DEC_B;        // L1 decode table index bits
 constexpr int kF = CUSZ_AMD_DEC_F;           // decode steps between ring refills
 constexpr int kDecWaves = CUSZ_AMD_DEC_WAVES;  // waves per workgroup (one workgroup per CU)
@@ -1107,6 +1110,9 @@ __device__ __forceinline__ void recon_block(const uint16_t* tile, T* out, size_t
     for (int z = 0; z < 8; z++) {
       if ((uint32_t)z >= nzv) break;
       const T o = t[z];
+#ifdef CUSZ_AMD_EXP_NOSTORE
+      if (true) { asm volatile("" ::"v"(o)); continue; }
+#endif
       if constexpr (BUF)
         buf_store<T>(o, ro, voff, (uint32_t)(((size_t)z * plane + (size_t)y * lx) * sizeof(T)));
       else
@@ -1266,13 +1272,20 @@ __device__ __forceinline__ void decode_chunks(const hfd::LdsTables<kDecB>& tb, c
         }
       }
     };
-    // a group is written into the ring two refills after its load; the first wait of a block
-    // comes 2 kF steps after the previous block's stores
+#if CUSZ_AMD_DEC_G == 4
+    // four groups in flight: a group is written into the ring four refills after its load
+    u32x4 pc4, pd4;
+    bool fc = false, fd = false;
     issue(pa, fa);
     quarter();
     issue(pb, fb);
     quarter();
-    do {
+    issue(pc4, fc);
+    quarter();
+    issue(pd4, fd);
+    quarter();
+    bool odd = false;
+    for (;;) {
       consume(pa, fa);
       issue(pa, fa);
       quarter();
@@ -1280,10 +1293,51 @@ __device__ __forceinline__ void decode_chunks(const hfd::LdsTables<kDecB>& tb, c
       issue(pb, fb);
       quarter();
       BPROF(pc[5]++;)
+      if (!__builtin_amdgcn_ballot_w64(cnt < target)) { odd = true; break; }
+      consume(pc4, fc);
+      issue(pc4, fc);
+      quarter();
+      consume(pd4, fd);
+      issue(pd4, fd);
+      quarter();
+      BPROF(pc[5]++;)
+      if (!__builtin_amdgcn_ballot_w64(cnt < target)) break;
+    }
+    BPROF(hfd::wave_sync(); tk = __builtin_readcyclecounter(); pc[2] += tk - tp; tp = tk;)
+    if (odd) {  // in flight, oldest first: c, d, a, b
+      consume(pc4, fc);
+      consume(pd4, fd);
+    }
+    consume(pa, fa);
+    consume(pb, fb);
+    if (!odd) {
+      consume(pc4, fc);
+      consume(pd4, fd);
+    }
+#else
+    // a group is written into the ring two refills after its load; the first wait of a block
+    // comes 2 kF steps after the previous block's stores
+    issue(pa, fa);
+    quarter();
+    issue(pb, fb);
+    quarter();
+    do {
+      BPROF(unsigned long long tc0 = __builtin_readcyclecounter();)
+      consume(pa, fa);
+      BPROF(hfd::wave_sync(); pc[10] += __builtin_readcyclecounter() - tc0;)
+      issue(pa, fa);
+      quarter();
+      BPROF(tc0 = __builtin_readcyclecounter();)
+      consume(pb, fb);
+      BPROF(hfd::wave_sync(); pc[10] += __builtin_readcyclecounter() - tc0;)
+      issue(pb, fb);
+      quarter();
+      BPROF(pc[5]++;)
     } while (__builtin_amdgcn_ballot_w64(cnt < target));
     BPROF(hfd::wave_sync(); tk = __builtin_readcyclecounter(); pc[2] += tk - tp; tp = tk;)
     consume(pa, fa);  // drain: nothing stays in flight across the stores below
     consume(pb, fb);
+#endif
     hfd::wave_sync();
     BPROF(tk = __builtin_readcyclecounter(); pc[3] += tk - tp; tp = tk;)
     // symbols decoded past the block end move to its front; they
@@ -1396,6 +1450,9 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
     };
     auto recon = [&](int blk) {
       if (blk == (int)(W / kBlk) - 1) prefetch(nx);  // the next brick (fetched during this block)
+#ifdef CUSZ_AMD_EXP_NORECON3
+      if (blk < 100) return;
+#endif
       const uint32_t nyv = min(8u, ly - y0), nzv = min(8u, lz - z0);
       const size_t base_elem = (size_t)z0 * plane + (size_t)y0 * lx + (size_t)bx * W + (size_t)blk * kBlk;
       if (ranked)

@@ -81,43 +81,45 @@ extern "C" int psz_amd_merge_archives(const uint8_t* const* parts, const size_t*
                                       const size_t* elem_offsets, psz_len full_len, uint8_t* out, size_t out_cap,
                                       size_t* out_bytes)
 {
-  if (!parts || !part_bytes || nparts < 1 || !out_bytes) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if (!parts || !part_bytes || nparts < 1 || !out_bytes) return PSZ_AMD_ERR_INVALID_ARG;
   std::vector<Part> P((size_t)nparts);
   size_t n_total = 0, splen = 0, ncell = 0, pardeg = 0;
   unsigned long long nbit = 0;
   for (int i = 0; i < nparts; i++) {
     Part& p = P[(size_t)i];
-    if (!parts[i] || part_bytes[i] < sizeof(psz_header)) return PSZ_ABORT_NOT_IMPLEMENTED;
+    if (!parts[i]) return PSZ_AMD_ERR_INVALID_ARG;
+    if (part_bytes[i] < sizeof(psz_header)) return PSZ_AMD_ERR_BAD_ARCHIVE;
     std::memcpy(&p.h, parts[i], sizeof(psz_header));
     const uint32_t* e = p.h.entry;
     // anchors (spline) are per-slab 8^3 lattices: not mergeable by concatenation
     if (e[PSZHEADER_ANCHOR] != e[PSZHEADER_ENCODED]) return PSZ_ABORT_NO_SUCH_PREDICTOR;
     if (e[PSZHEADER_ENC_PASS2_END] > part_bytes[i] || e[PSZHEADER_ENCODED] + sizeof(phf_header) > part_bytes[i])
-      return PSZ_ABORT_NOT_IMPLEMENTED;
+      return PSZ_AMD_ERR_BAD_ARCHIVE;
     for (int k = 1; k <= PSZHEADER_ENC_PASS2_END; k++)
-      if (e[k] < e[k - 1]) return PSZ_ABORT_NOT_IMPLEMENTED;
+      if (e[k] < e[k - 1]) return PSZ_AMD_ERR_BAD_ARCHIVE;
     p.base = parts[i];
     p.phf = parts[i] + e[PSZHEADER_ENCODED];
     std::memcpy(&p.ph, p.phf, sizeof(phf_header));
     p.n = p.h.len.x * p.h.len.y * p.h.len.z;
     // the part's own segments: outlier cells, phf sections inside the phf segment, chunk table
-    if ((size_t)e[PSZHEADER_ENC_PASS1_END] - e[PSZHEADER_SPFMT] != 8 * p.h.splen) return PSZ_ABORT_NOT_IMPLEMENTED;
-    if (!phf_sections_ok(p, e[PSZHEADER_SPFMT] - e[PSZHEADER_ENCODED])) return PSZ_ABORT_NOT_IMPLEMENTED;
+    if ((size_t)e[PSZHEADER_ENC_PASS1_END] - e[PSZHEADER_SPFMT] != 8 * p.h.splen) return PSZ_AMD_ERR_BAD_ARCHIVE;
+    if (!phf_sections_ok(p, e[PSZHEADER_SPFMT] - e[PSZHEADER_ENCODED])) return PSZ_AMD_ERR_BAD_ARCHIVE;
     const Part& q = P[0];
     if (p.h.dtype != q.h.dtype || p.h.pipeline.predictor != q.h.pipeline.predictor || p.h.rc.radius != q.h.rc.radius ||
         p.h.rc.eb != q.h.rc.eb || p.ph.bklen != q.ph.bklen || p.ph.sublen != q.ph.sublen)
-      return PSZ_ABORT_NOT_IMPLEMENTED;
+      return p.h.dtype != q.h.dtype ? PSZ_ABORT_UNSUPPORTED_TYPE : PSZ_AMD_ERR_INVALID_ARG;  // parts of different runs
     const size_t rv = rvbk_bytes(p.ph.bklen);
-    if (p.ph.entry[PHFHEADER_END] + e[PSZHEADER_ENCODED] > part_bytes[i]) return PSZ_ABORT_NOT_IMPLEMENTED;
+    if (p.ph.entry[PHFHEADER_END] + e[PSZHEADER_ENCODED] > part_bytes[i]) return PSZ_AMD_ERR_BAD_ARCHIVE;
     if (std::memcmp(p.phf + PHFHEADER_FORCED_ALIGN, q.phf + PHFHEADER_FORCED_ALIGN, rv) != 0)
-      return PSZ_ABORT_NOT_IMPLEMENTED;  // slabs were not compressed with one shared codebook
+      return PSZ_AMD_ERR_INVALID_ARG;  // slabs were not compressed with one shared codebook
     // every slab but the last must end on a chunk boundary, or the merged chunking differs
-    if (p.ph.sublen <= 0 || (i + 1 < nparts && p.n % (size_t)p.ph.sublen != 0)) return PSZ_ABORT_NOT_IMPLEMENTED;
+    if (p.ph.sublen <= 0) return PSZ_AMD_ERR_BAD_ARCHIVE;
+    if (i + 1 < nparts && p.n % (size_t)p.ph.sublen != 0) return PSZ_ABORT_UNSUPPORTED_DIMENSION;
     // slabs split the slowest axis of the field: the faster extents must be the field's, and
     // every slab but the last must end on a prediction-tile boundary (z: 8 planes, 2-D: 32 rows,
     // 1-D: 1024 elements; launch.hh:47-121), or Lorenzo would cross the seam differently
     if (!slab_shape_ok(p.h.len, full_len, i + 1 == nparts)) return PSZ_ABORT_UNSUPPORTED_DIMENSION;
-    if (elem_offsets && elem_offsets[i] != n_total) return PSZ_ABORT_NOT_IMPLEMENTED;  // slabs in field order
+    if (elem_offsets && elem_offsets[i] != n_total) return PSZ_AMD_ERR_INVALID_ARG;  // slabs in field order
     n_total += p.n;
     splen += p.h.splen;
     ncell += p.ph.total_ncell;
@@ -157,7 +159,8 @@ extern "C" int psz_amd_merge_archives(const uint8_t* const* parts, const size_t*
   }
   const size_t total = h.entry[PSZHEADER_ENC_PASS2_END];
   *out_bytes = total;
-  if (!out || out_cap < total) return PSZ_ABORT_NOT_IMPLEMENTED;  // *out_bytes tells the size needed
+  if (!out) return PSZ_SUCCESS;  // size query
+  if (out_cap < total) return PSZ_AMD_ERR_INVALID_ARG;
 
   uint8_t* phf = out + h.entry[PSZHEADER_ENCODED];
   std::memcpy(out, &h, sizeof(h));

@@ -39,7 +39,7 @@ int report_hip_error(hipError_t e, const char* expr, const char* file, int line)
 {
   std::fprintf(stderr, "[cusz_amd] HIP error %d (%s) at %s:%d: %s\n", (int)e, hipGetErrorString(e), file, line,
                expr);
-  return PSZ_ABORT_NOT_IMPLEMENTED;  // closest psz_error_status for a runtime failure
+  return PSZ_AMD_ERR_DEVICE;
 }
 
 static int ndim_of(psz_len l)
@@ -79,7 +79,7 @@ struct Pipeline {
   LorenzoGeom geom{};
   BrickLaunch bl{};               // fused brick path (brick.hip); bl.g.ok when eligible
   int layout = 0;                 // PSZ_AMD_LAYOUT_*: 0 brick layout when eligible, 1 reference layout
-  bool layout_set = false;        // the caller chose the layout (psz_amd_set_layout)
+  bool layout_set = false;        // PSZ_AMD_LAYOUT_BRICK_FORCE: bricks also for small 2-D fields
   int codebook = 0;               // PSZ_AMD_CODEBOOK_*: exact (full histogram) or sampled (one pass)
   uint16_t* d_bhist = nullptr;    // per-brick u16 histograms (pass 1 -> reservation)
   uint32_t* d_ub = nullptr;       // per-brick region upper bounds (cells)
@@ -291,7 +291,7 @@ struct Pipeline {
       __builtin_ia32_pause();
     }
     CUSZ_AMD_HIP_CHECK(hipStreamSynchronize(stream));
-    return __atomic_load_n(flag(fl), __ATOMIC_ACQUIRE) == e ? PSZ_SUCCESS : PSZ_ABORT_NOT_IMPLEMENTED;
+    return __atomic_load_n(flag(fl), __ATOMIC_ACQUIRE) == e ? PSZ_SUCCESS : PSZ_AMD_ERR_DEVICE;
   }
 
   static XferRegions regions(std::initializer_list<std::tuple<void*, const void*, size_t>> l)
@@ -357,7 +357,7 @@ struct Pipeline {
     }
     const int radius = h->rc.radius;
     const int bklen = 2 * radius;
-    if (radius < 1 || bklen > kMaxBklen) return PSZ_ABORT_NOT_IMPLEMENTED;
+    if (radius < 1 || bklen > kMaxBklen) return PSZ_AMD_ERR_INVALID_ARG;
 
     const bool brick = use_brick(pred);
     // chunk length: the caller's, else the tuned one
@@ -449,7 +449,7 @@ struct Pipeline {
   // slabs) -> encode -> archive.
   int compress_finish(psz_header* h, const uint32_t* ext_hist, uint8_t** out, size_t* outlen)
   {
-    if (!pend.active) return PSZ_ABORT_NOT_IMPLEMENTED;
+    if (!pend.active) return PSZ_AMD_ERR_STATE;
     pend.active = false;
     const int radius = pend.radius, bklen = 2 * radius;
     if (ext_hist) {
@@ -619,7 +619,7 @@ struct Pipeline {
     if (h->pipeline.codec1 != Huffman) return PSZ_ABORT_NO_SUCH_CODEC;
     const bool zz = h->pipeline.predictor == LorenzoZigZag;
     const int radius = h->rc.radius, bklen = 2 * radius;
-    if (radius < 1 || bklen > kMaxBklen) return PSZ_ABORT_NOT_IMPLEMENTED;
+    if (radius < 1 || bklen > kMaxBklen) return PSZ_AMD_ERR_INVALID_ARG;
     const BrickGeom& g = bl.g;
     mark(0);
     if (h->rc.mode == Rel) {  // libcusz.cc:287-293
@@ -720,7 +720,7 @@ struct Pipeline {
 #endif
     if (tmo) {
       std::fprintf(stderr, "[cusz_amd] encoder reservation/look-back check failed\n");
-      return PSZ_ABORT_NOT_IMPLEMENTED;
+      return PSZ_AMD_ERR_ENCODER;
     }
     if (ci.outlier_lost) return PSZ_WARN_OUTLIER_TOO_MANY;
     *out = d_archive;
@@ -730,6 +730,8 @@ struct Pipeline {
 
   int decode_codes(const psz_header* h, const uint8_t* in)
   {
+    // the decoders write d_codes, which a pending compress_finish would pack (as decompress)
+    pend.active = false;
     const int bklen = 2 * h->rc.radius;
     const size_t phf_off = h->entry[PSZHEADER_ENCODED];
     const size_t rvbk = rvbk_bytes(bklen);
@@ -973,7 +975,7 @@ int psz_release_resource(psz_resource* m)
 template <typename T>
 static int compress_impl(psz_resource* m, psz_rc2 rc, T* in, psz_header* out_h, uint8_t** out, size_t* outlen)
 {
-  if (!m || !in || !out || !outlen) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if (!m || !in || !out || !outlen) return PSZ_AMD_ERR_INVALID_ARG;
   Pipeline* p = cusz_amd::P(m);
   if ((sizeof(T) == 4) != (m->header->dtype == F4)) return PSZ_ABORT_UNSUPPORTED_TYPE;
   int status = PSZ_SUCCESS;
@@ -994,7 +996,7 @@ static int compress_impl(psz_resource* m, psz_rc2 rc, T* in, psz_header* out_h, 
 template <typename T>
 static int scan_impl(psz_resource* m, psz_rc2 rc, T* in)
 {
-  if (!m || !in) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if (!m || !in) return PSZ_AMD_ERR_INVALID_ARG;
   Pipeline* p = cusz_amd::P(m);
   if ((sizeof(T) == 4) != (m->header->dtype == F4)) return PSZ_ABORT_UNSUPPORTED_TYPE;
   int status = PSZ_SUCCESS;
@@ -1012,7 +1014,7 @@ static int scan_impl(psz_resource* m, psz_rc2 rc, T* in)
 static int export_hist(psz_resource* m, uint32_t* d_out, int status)
 {
   Pipeline* p = cusz_amd::P(m);
-  if (!d_out) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if (!d_out) return PSZ_AMD_ERR_INVALID_ARG;
   CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(d_out, p->d_hist, sizeof(uint32_t) * 2 * m->header->rc.radius,
                                     hipMemcpyDeviceToDevice, p->stream));
   return status;
@@ -1034,7 +1036,7 @@ int psz_compress_double(psz_resource* m, psz_rc2 rc, double* in, psz_header* out
 int psz_compress_analyize_float(psz_resource* m, psz_rc2 rc, float* in, u4* exported_h_hist)
 {
   // compressor.inl:305-337: predict + histogram only, the histogram exported to the host
-  if (!exported_h_hist) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if (!exported_h_hist) return PSZ_AMD_ERR_INVALID_ARG;
   const int s = scan_impl<float>(m, rc, in);
   if (s != PSZ_SUCCESS && s != PSZ_WARN_RADIUS_TOO_LARGE) return s;
   Pipeline* p = cusz_amd::P(m);
@@ -1061,7 +1063,7 @@ int psz_amd_compress_scan_double(psz_resource* m, psz_rc2 rc, double* in, uint32
 int psz_amd_value_range(psz_resource* m, const void* in, size_t len, double* d_minmax)
 {
   Pipeline* p = cusz_amd::P(m);
-  if (!p || !in || !d_minmax) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if (!p || !in || !d_minmax) return PSZ_AMD_ERR_INVALID_ARG;
   if (len == 0) len = p->n;
   CUSZ_AMD_HIP_CHECK(hipSetDevice(p->device));
   if (m->header->dtype == F4)
@@ -1077,7 +1079,7 @@ int psz_amd_compress_finish(psz_resource* m, const uint32_t* d_hist, psz_header*
                             size_t* outlen)
 {
   Pipeline* p = cusz_amd::P(m);
-  if (!p || !out || !outlen) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if (!p || !out || !outlen) return PSZ_AMD_ERR_INVALID_ARG;
   CUSZ_AMD_HIP_CHECK(hipSetDevice(p->device));
   const int s = p->compress_finish(m->header, d_hist, out, outlen);
   if (out_h) *out_h = *m->header;
@@ -1089,14 +1091,14 @@ int psz_amd_compress_finish(psz_resource* m, const uint32_t* d_hist, psz_header*
 template <typename T>
 static int decompress_impl(psz_resource* m, uint8_t* in, size_t in_len, T* out)
 {
-  if (!m || !in || !out) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if (!m || !in || !out) return PSZ_AMD_ERR_INVALID_ARG;
   Pipeline* p = cusz_amd::P(m);
   // the header's segment table must be ordered and fit the archive the caller passed
   const uint32_t* e = m->header->entry;
   for (int k = 1; k <= PSZHEADER_ENC_PASS2_END; k++)
-    if (e[k] < e[k - 1]) return PSZ_ABORT_NOT_IMPLEMENTED;
-  if (in_len && e[PSZHEADER_ENC_PASS2_END] > in_len) return PSZ_ABORT_NOT_IMPLEMENTED;
-  if ((size_t)e[PSZHEADER_ENC_PASS1_END] - e[PSZHEADER_SPFMT] != 8 * m->header->splen) return PSZ_ABORT_NOT_IMPLEMENTED;
+    if (e[k] < e[k - 1]) return PSZ_AMD_ERR_BAD_ARCHIVE;
+  if (in_len && e[PSZHEADER_ENC_PASS2_END] > in_len) return PSZ_AMD_ERR_BAD_ARCHIVE;
+  if ((size_t)e[PSZHEADER_ENC_PASS1_END] - e[PSZHEADER_SPFMT] != 8 * m->header->splen) return PSZ_AMD_ERR_BAD_ARCHIVE;
   if ((sizeof(T) == 4) != (m->header->dtype == F4)) return PSZ_ABORT_UNSUPPORTED_TYPE;
   CUSZ_AMD_HIP_CHECK(hipSetDevice(p->device));
   int s = p->decompress<T>(m->header, in, out);
@@ -1123,7 +1125,7 @@ int psz_decompress_double(psz_resource* m, uint8_t* in, size_t const in_len, dou
 int psz_amd_get_internals(psz_resource* m, psz_amd_internals* o)
 {
   Pipeline* p = cusz_amd::P(m);
-  if (!p || !o) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if (!p || !o) return PSZ_AMD_ERR_INVALID_ARG;
   o->d_quant_codes = p->d_codes;
   o->d_hist = p->d_hist;
   o->d_book = p->d_book;
@@ -1142,7 +1144,7 @@ int psz_amd_get_internals(psz_resource* m, psz_amd_internals* o)
 int psz_amd_enable_timing(psz_resource* m, int on)
 {
   Pipeline* p = cusz_amd::P(m);
-  if (!p) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if (!p) return PSZ_AMD_ERR_INVALID_ARG;
   p->timing = on != 0;
   return PSZ_SUCCESS;
 }
@@ -1150,7 +1152,7 @@ int psz_amd_enable_timing(psz_resource* m, int on)
 int psz_amd_stage_times(psz_resource* m, float* ms, int n)
 {
   Pipeline* p = cusz_amd::P(m);
-  if (!p || !ms) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if (!p || !ms) return PSZ_AMD_ERR_INVALID_ARG;
   for (int i = 0; i < n && i < PSZ_AMD_T_COUNT; i++) ms[i] = p->stage_ms[i];
   return PSZ_SUCCESS;
 }
@@ -1158,11 +1160,11 @@ int psz_amd_stage_times(psz_resource* m, float* ms, int n)
 int psz_amd_set_sublen(psz_resource* m, int sublen)
 {
   Pipeline* p = cusz_amd::P(m);
-  if (!p || sublen < 0) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if (!p || sublen < 0) return PSZ_AMD_ERR_INVALID_ARG;
   p->user_sublen = sublen;
   if (sublen == 0) {
     cusz_amd::tune_chunking(p->n, p->device, &p->sublen, &p->pardeg);
-    if (p->alloc_chunk_state() != hipSuccess) return PSZ_ABORT_NOT_IMPLEMENTED;
+    if (p->alloc_chunk_state() != hipSuccess) return PSZ_AMD_ERR_DEVICE;
   }
   return PSZ_SUCCESS;
 }
@@ -1170,7 +1172,7 @@ int psz_amd_set_sublen(psz_resource* m, int sublen)
 int psz_amd_set_decoder(psz_resource* m, int kind)
 {
   Pipeline* p = cusz_amd::P(m);
-  if (!p || kind < PSZ_AMD_DECODER_AUTO || kind > PSZ_AMD_DECODER_WAVE) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if (!p || kind < PSZ_AMD_DECODER_AUTO || kind > PSZ_AMD_DECODER_WAVE) return PSZ_AMD_ERR_INVALID_ARG;
   p->decoder = kind;
   return PSZ_SUCCESS;
 }
@@ -1178,7 +1180,7 @@ int psz_amd_set_decoder(psz_resource* m, int kind)
 int psz_amd_set_codebook(psz_resource* m, int mode)
 {
   Pipeline* p = cusz_amd::P(m);
-  if (!p || (mode != PSZ_AMD_CODEBOOK_EXACT && mode != PSZ_AMD_CODEBOOK_SAMPLED)) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if (!p || (mode != PSZ_AMD_CODEBOOK_EXACT && mode != PSZ_AMD_CODEBOOK_SAMPLED)) return PSZ_AMD_ERR_INVALID_ARG;
   p->codebook = mode;
   return PSZ_SUCCESS;
 }
@@ -1186,16 +1188,18 @@ int psz_amd_set_codebook(psz_resource* m, int mode)
 int psz_amd_set_layout(psz_resource* m, int layout)
 {
   Pipeline* p = cusz_amd::P(m);
-  if (!p || (layout != PSZ_AMD_LAYOUT_BRICK && layout != PSZ_AMD_LAYOUT_REFERENCE)) return PSZ_ABORT_NOT_IMPLEMENTED;
-  p->layout = layout;
-  p->layout_set = true;
+  if (!p) return PSZ_AMD_ERR_INVALID_ARG;
+  if (layout != PSZ_AMD_LAYOUT_BRICK && layout != PSZ_AMD_LAYOUT_REFERENCE && layout != PSZ_AMD_LAYOUT_BRICK_FORCE)
+    return PSZ_AMD_ERR_INVALID_ARG;
+  p->layout = layout == PSZ_AMD_LAYOUT_REFERENCE ? PSZ_AMD_LAYOUT_REFERENCE : PSZ_AMD_LAYOUT_BRICK;
+  p->layout_set = layout == PSZ_AMD_LAYOUT_BRICK_FORCE;  // BRICK keeps the small-2-D default
   return PSZ_SUCCESS;
 }
 
 int psz_amd_decode_codes(psz_resource* m, uint8_t* in)
 {
   Pipeline* p = cusz_amd::P(m);
-  if (!p || !in) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if (!p || !in) return PSZ_AMD_ERR_INVALID_ARG;
   return p->decode_codes(m->header, in);
 }
 
@@ -1205,7 +1209,7 @@ const char* psz_amd_version(void) { return "cusz_amd 0.1 (gfx950)"; }
 int cusz_amd_set_stream(psz_resource* m, void* stream)
 {
   Pipeline* p = cusz_amd::P(m);
-  if (!p) return PSZ_ABORT_NOT_IMPLEMENTED;
+  if (!p) return PSZ_AMD_ERR_INVALID_ARG;
   p->stream = (hipStream_t)stream;
   m->stream = stream;
   return PSZ_SUCCESS;

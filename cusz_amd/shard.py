@@ -100,6 +100,21 @@ def allreduce_histograms(hists, dist):
     return hists
 
 
+def check_streams(resources, device) -> None:
+    """The sharded helpers order their phases by torch's current stream only (no host sync, no
+    events): every manager must run on that stream, or the all-reduce could read histograms
+    (or extrema) the scans have only partly written.  Raise instead of corrupting silently."""
+    import torch
+
+    if device is None or torch.device(device).type != "cuda":
+        return
+    cur = torch.cuda.current_stream(device).cuda_stream
+    for r in resources:
+        if getattr(r, "stream", cur) != cur:
+            raise ValueError(f"manager stream {r.stream:#x} is not torch's current stream {cur:#x}: "
+                             "create the Resource with stream=torch.cuda.current_stream().cuda_stream")
+
+
 def global_value_ranges(resources, fields, dist):
     """Rel (r2r) mode across slabs: max - min of every field over all ranks.  Each slab's range
     comes from the library's extrema kernel (psz_amd_value_range: extrema.cuhip.inl:150-208, on
@@ -107,6 +122,7 @@ def global_value_ranges(resources, fields, dist):
     (libcusz.cc:287-293 computes this range per field on one GPU)."""
     import torch
 
+    check_streams(resources, fields[0].device)
     mm = torch.empty((len(fields), 2), dtype=torch.float64, device=fields[0].device)
     for i, (r, f) in enumerate(zip(resources, fields)):
         r.value_range(f.data_ptr(), mm[i].data_ptr(), f.numel())
@@ -122,15 +138,16 @@ def compress_fields_sharded(resources, fields, eb, dist, mode=0, radius=512, dev
     [fields, bklen] histograms, then finish every slab.  Rel mode: eb times the field's global
     value range (one more all-reduce), the slabs then compress with that absolute bound.
 
-    The managers must run on the caller's current stream (torch.cuda.current_stream): RCCL
-    orders the all-reduce after the scans and the finish after the all-reduce on that stream,
-    so no host synchronisation is needed between the phases.  The u32 histogram sums are
+    The managers must run on the caller's current stream (torch.cuda.current_stream; checked,
+    ValueError otherwise): RCCL orders the all-reduce after the scans and the finish after the
+    all-reduce on that stream, so no host synchronisation is needed between the phases.  The u32 histogram sums are
     reduced as int32 (the bit pattern is the u32 sum: every count is < 2^32).
     Returns [(archive_ptr, nbytes)] (device archives, valid until the manager's next compress)."""
     import torch
 
     bklen = 2 * radius
     f = len(resources)
+    check_streams(resources, device if device is not None else (fields[0].device if fields else None))
     ebs = [eb * r for r in global_value_ranges(resources, fields, dist)] if mode == 1 else [eb] * f
     if hists is None:
         hists = torch.empty((f, bklen), dtype=torch.int32, device=device)

@@ -2,7 +2,7 @@
  *
  * None of these exist in the reference; they expose what the MI355X build measures and
  * what the parity tests need (stage timings, intermediate device buffers, tuning knobs,
- * slab sharding helpers for multi-GPU runs).  All functions return psz_error_status codes.
+ * slab sharding helpers for multi-GPU runs).  All functions return the status codes below.
  */
 #ifndef CUSZ_AMD_EXT_H
 #define CUSZ_AMD_EXT_H
@@ -15,6 +15,16 @@ extern "C" {
 #include <stdint.h>
 
 #include "cusz/context.h"
+
+/* Status codes.  Every entry point returns a psz_error_status value (cusz/type.h: the reference's
+ * values, used where one applies: PSZ_ABORT_UNSUPPORTED_TYPE for a dtype mismatch,
+ * PSZ_ABORT_UNSUPPORTED_DIMENSION for an archive of another shape, ...) or one of these, for
+ * failures the reference enum has no value for (it reports them as crashes or exceptions): */
+#define PSZ_AMD_ERR_INVALID_ARG 100 /* null handle or pointer, a size or knob value out of range   */
+#define PSZ_AMD_ERR_BAD_ARCHIVE 101 /* archive or header malformed, truncated or inconsistent      */
+#define PSZ_AMD_ERR_DEVICE 102      /* a HIP runtime call, allocation or kernel launch failed       */
+#define PSZ_AMD_ERR_STATE 103       /* call out of order (compress_finish without a pending scan)   */
+#define PSZ_AMD_ERR_ENCODER 104     /* the encoder's own overflow / look-back check failed (a bug)  */
 
 /* Stage indices for psz_amd_stage_times (milliseconds of the last call, HIP events on the
  * manager's stream; only filled after psz_amd_enable_timing(m, 1)). */
@@ -77,6 +87,9 @@ int psz_amd_set_decoder(psz_resource* m, int kind);
  *  REFERENCE: chunks in index order, no gaps (byte-identical to the reference encoder). */
 #define PSZ_AMD_LAYOUT_BRICK 0
 #define PSZ_AMD_LAYOUT_REFERENCE 1
+/* BRICK_FORCE: the brick layout also for small 2-D fields (BRICK keeps the reference layout for
+ * 2-D fields with fewer than 4 bricks per CU, where it is faster). */
+#define PSZ_AMD_LAYOUT_BRICK_FORCE 2
 int psz_amd_set_layout(psz_resource* m, int layout);
 
 /* Codebook source (brick layout, 3-D fields; other fields always use EXACT).
@@ -116,8 +129,11 @@ int psz_amd_value_range(psz_resource* m, const void* IN_d_data, size_t IN_len, d
  * into the archive of the whole field: the archive one process would have written for it
  * (chunks concatenated, par_entry rebased by the cells before each slab, outlier indices by
  * the slab's element offset).  elem_offsets (may be NULL) are checked against the running
- * sum.  *out_bytes receives the merged size even when out_cap is too small (then nonzero is
- * returned and nothing is written). */
+ * sum.  *out_bytes receives the merged size; with out == NULL that is all (a size query,
+ * PSZ_SUCCESS); with out_cap too small nothing is written and PSZ_AMD_ERR_INVALID_ARG is
+ * returned.  Malformed parts: PSZ_AMD_ERR_BAD_ARCHIVE; parts that are not tile-aligned slabs of
+ * the field: PSZ_ABORT_UNSUPPORTED_DIMENSION; parts of different runs (codebook, eb, dtype):
+ * PSZ_AMD_ERR_INVALID_ARG / PSZ_ABORT_UNSUPPORTED_TYPE. */
 int psz_amd_merge_archives(const uint8_t* const* parts, const size_t* part_bytes, int nparts,
                            const size_t* elem_offsets, psz_len full_len, uint8_t* out, size_t out_cap,
                            size_t* out_bytes);

@@ -41,6 +41,8 @@ for i, nm in [(1, "start"), (2, "decode"), (3, "drain"), (4, "recon")]:
     print(f"  {nm:7s} {v[i] / nbk:10.0f} cycles/brick")
 print(f"  loop iterations {v[5] / nbk:.1f}/brick ({v[5] / nbk * 2 * 4:.0f} wave-steps, kF = 4)")
 print(f"  lane-steps: done {v[7] / nbk:.0f}/brick, starved {v[6] / nbk:.0f}/brick")
+if v[10]:
+    print(f"  3-D ring refill waits {v[10] / nbk:.0f} cycles/brick")
 if v[8] or v[9]:
     print(f"  1-D recon: values {v[8] / nbk:.0f}, scans + stores {v[9] / nbk:.0f} cycles/brick")
 print(f"max err {(y.double() - x.double()).abs().max().item():.3e}")

@@ -72,7 +72,7 @@ def _field(kind, dims, dtype, seed):
 def test_brick_parity(oracle, dims, dtype, eb, zz, radius, kind):
     data = _field(kind, dims, dtype, seed=sum(dims))
     # 2-D fields this small take the reference layout by default (too few bricks): force bricks
-    layout = cz.LAYOUT_BRICK if dims[1] > 1 and dims[2] == 1 else None
+    layout = cz.LAYOUT_BRICK_FORCE if dims[1] > 1 and dims[2] == 1 else None
     arch, a = run_roundtrip(oracle, data, dims, eb, dtype, zz, radius, check_bound=kind != "noise", layout=layout)
     assert a["sublen"] == 256, "brick layout expected"
 

@@ -132,8 +132,9 @@ def test_merge_rejects_mismatched_codebooks(oracle):
         codes, ov, oi = oracle.lorenzo_c(data[s.offset:s.offset + s.count], s.dims, 1e-4)
         book, rv = oracle.codebook(oracle.histogram(codes))  # per-slab books: not mergeable
         parts.append(oracle_archive(oracle, codes, ov, oi, s.dims, 1e-4, book, rv, sublen=256))
-    with pytest.raises(cz.PszError):
+    with pytest.raises(cz.PszError) as e:
         cz.merge_archives(parts, dims)
+    assert e.value.status == cz.PSZ_AMD_ERR_INVALID_ARG
 
 
 @pytest.mark.parametrize("dims,cut", [((64, 40, 16), 4), ((300, 64, 1), 16), ((4096, 1, 1), 512)])
@@ -157,8 +158,9 @@ def test_merge_rejects_slabs_off_tile_boundaries(oracle, dims, cut):
         codes, ov, oi = oracle.lorenzo_c(data[off:off + cnt], d, 1e-4)
         parts.append(oracle_archive(oracle, codes, ov, oi, d, 1e-4, book, rv, sublen=256))
         off += cnt
-    with pytest.raises(cz.PszError):
+    with pytest.raises(cz.PszError) as e:
         cz.merge_archives(parts, dims)
+    assert e.value.status == cz.PSZ_ABORT_UNSUPPORTED_DIMENSION
 
 
 def test_merge_rejects_wrong_slab_extent(oracle):
@@ -171,5 +173,22 @@ def test_merge_rejects_wrong_slab_extent(oracle):
     codes, ov, oi = oracle.lorenzo_c(data, d, 1e-4)
     book, rv = oracle.codebook(oracle.histogram(codes))
     p = oracle_archive(oracle, codes, ov, oi, d, 1e-4, book, rv, sublen=256)
-    with pytest.raises(cz.PszError):
+    with pytest.raises(cz.PszError) as e:
         cz.merge_archives([p, p], dims)
+    assert e.value.status == cz.PSZ_ABORT_UNSUPPORTED_DIMENSION
+
+
+def test_merge_rejects_truncated_part(oracle):
+    """A part shorter than its own header's segment table says is a malformed archive, told apart
+    from a well-formed part of the wrong shape by its status."""
+    import cusz_amd as cz
+
+    dims = (64, 40, 16)
+    data = datagen.smooth3d_np(dims, 5)
+    codes, ov, oi = oracle.lorenzo_c(data, dims, 1e-4)
+    book, rv = oracle.codebook(oracle.histogram(codes))
+    p = oracle_archive(oracle, codes, ov, oi, dims, 1e-4, book, rv, sublen=256)
+    for cut in (len(p) - 8, 100):
+        with pytest.raises(cz.PszError) as e:
+            cz.merge_archives([p[:cut]], dims)
+        assert e.value.status == cz.PSZ_AMD_ERR_BAD_ARCHIVE
