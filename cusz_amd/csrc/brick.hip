@@ -1165,9 +1165,13 @@ __global__ void __launch_bounds__(256) k_brick_cell_bounds(const uint32_t* __res
 #ifdef CUSZ_AMD_DEC_PROFILE
 #define BPROF_P , unsigned long long(&pc)[16], unsigned long long &tk, unsigned long long &tp
 #define BPROF_A , pc, tk, tp
+#define BPROF_A4 , pc, tk, tp
+#define BPROF_P4 , unsigned long long(&pc)[16], unsigned long long &tk, unsigned long long &tp0
 #else
+#define BPROF_P4
 #define BPROF_P
 #define BPROF_A
+#define BPROF_A4
 #endif
 
 // One wave's decoder state that outlives a chunk: bitstream resource, the lane's ring column, the
@@ -1355,25 +1359,193 @@ __device__ __forceinline__ void decode_chunks(const hfd::LdsTables<kDecB>& tb, c
   }
 }
 
+// ---- compact decoder (3-D fused path) ---------------------------------------------------------
+// The same chunk decode as decode_chunks with fewer instructions per step (the loop is bound by
+// how fast one wave issues its dependent chain, not by LDS or HBM bandwidth; round-4 counters:
+// 40 VALU + 6 LDS + 6 SALU per step before, ~15 + 4 after):
+//  * the window is read from the LDS ring each step: words J and J+1 by one ds_read2st64 (slot
+//    16 mirrors slot 0, so the pair never wraps), shifted by alignbit -- no window registers to
+//    rotate, no word-crossing test; 8 x (the lane's bit position + 511) masked by 0xF00 is the
+//    slot's byte offset, `npos` (= -position) the shift;
+//  * compact table entries (hfd::Tab4): the tile pointer advance, the bits and the symbols come
+//    out of the entry with one or two instructions each;
+//  * the state is the position and the tile pointer: a lane takes part in a quarter while its
+//    pointer is below the block's limit and the ring holds every word the quarter can reach.
+// Smaller tables and tile (74 columns: 64 + the 9 overshoot) let 9 waves share a CU.
+constexpr int kTP4 = kBlk + 10;
+static_assert(((kTP4 / 2) & 1) == 1, "odd dword pitch");
+static_assert(kBlk + 2 * kF + 1 <= kTP4, "overshoot columns");
+constexpr uint32_t kRing4 = 16;                                // ring words per lane (+ mirror, junk)
+constexpr size_t kD4Tile = (size_t)(kRing4 + 2) * 256;          // slots 0..15, mirror 16, junk 17
+constexpr size_t kD4Cells = kD4Tile + (size_t)64 * kTP4 * 2;
+constexpr size_t kD4Rows = kD4Cells + (size_t)kCellCap * 4;
+constexpr size_t kD4WaveBytes = kD4Rows + (size_t)(65 + 64) * 4;
+#ifndef CUSZ_AMD_DEC4_WAVES
+#define CUSZ_AMD_DEC4_WAVES 9
+#endif
+constexpr int kDec4Waves = CUSZ_AMD_DEC4_WAVES;
+static_assert(sizeof(hfd::Tab4) + kDec4Waves * kD4WaveBytes <= 160 * 1024, "LDS");
+
+struct DecWave4 {
+  __amdgpu_buffer_rsrc_t rbits;
+  uint32_t* ring_lane;  // slot s of this lane at ring_lane[64 s]
+  uint16_t* tile;
+  uint32_t ubk;
+  int lane;
+};
+
+// One chunk per lane (bits at byte vbase, nbit bits, vlen <= W symbols; a dead lane decodes
+// nothing; its first 8 words in first[0..1]) in W / kBlk blocks into the tile; recon(blk) after
+// each block, blk_start(blk) before it, pro() while the first words are written.
+template <class Pro, class BlkStart, class Recon>
+__device__ __forceinline__ void decode_chunks4(const hfd::Tab4& tb, const hfd::DecRegs4& rg, const DecWave4& dw,
+                                               bool live, uint32_t vbase, uint32_t nbit, uint32_t vlen, Pro&& pro,
+                                               BlkStart&& blk_start, Recon&& recon BPROF_P4, uint32_t W,
+                                               const u32x4* first)
+{
+  const int lane = dw.lane;
+  uint32_t* const ring = dw.ring_lane;
+  const uint32_t nwords = live ? (nbit + 31u) >> 5 : 0u;
+  const u32x4 a0 = first[0], a1 = first[1];
+  pro();
+  ring[0] = a0.x, ring[64] = a0.y, ring[2 * 64] = a0.z, ring[3 * 64] = a0.w;
+  ring[4 * 64] = a1.x, ring[5 * 64] = a1.y, ring[6 * 64] = a1.z, ring[7 * 64] = a1.w;
+  ring[16 * 64] = a0.x;  // mirror of slot 0
+  uint32_t A = 0, Bw = a0.x;  // words J, J + 1 of the window (J = -1 at bit 0: junk, shift 0)
+  uint32_t pos8 = 8u * 511u, npos = 0;  // 8 x (chunk bit position + 511); -position (the shift)
+  uint32_t ltop = 8, ctop = 8;   // words requested / written to the ring
+  // a quarter reaches at most 4 x 16 + 27 bits: the lane steps only if their words are in
+  // (pos8 < 8 (32 ctop + 388))
+  uint32_t rdy = ctop >= nwords ? 0xFFFFFFFFu : 256u * ctop + 8u * 388u;
+  uint16_t* tp = dw.tile + lane * kTP4;
+  u32x4 pa, pb;  // groups in flight
+  bool fa = false, fb = false;
+  BPROF(hfd::wave_sync(); tk = __builtin_readcyclecounter(); pc[1] += tk - tp0; tp0 = tk;)
+
+  // next four words of the chunk, once their slots are free (words before J are)
+  auto issue = [&](u32x4& p, bool& f) {
+    const bool ok = ltop < nwords && ltop + 4u <= (pos8 >> 8);
+    p = __builtin_amdgcn_raw_buffer_load_b128(dw.rbits, (int)(ok ? vbase + ltop * 4u : kOOB), 0, 0);
+    f = ok;
+    ltop += ok ? 4u : 0u;
+  };
+  // a landed group into its slots (and the mirror)
+  auto consume = [&](const u32x4& p, bool& f) {
+    if (f) {
+      uint32_t* sl = ring + (ctop & (kRing4 - 1u)) * 64;
+      sl[0] = p.x, sl[64] = p.y, sl[128] = p.z, sl[192] = p.w;
+      if ((ctop & (kRing4 - 1u)) == 0u) ring[16 * 64] = p.x;
+      ctop += 4u;
+      rdy = ctop >= nwords ? 0xFFFFFFFFu : 256u * ctop + 8u * 388u;
+    }
+    f = false;
+  };
+  // the entry's symbols into the tile, the position forward, the next window read
+  auto advance = [&](uint32_t e) {
+    const uint32_t sy = e & hfd::kEnt4SymMask;
+    tp[0] = (uint16_t)sy;
+    asm volatile("" ::: "memory");  // two u16 stores: merged they would be an unaligned b32
+    tp[1] = (uint16_t)(sy >> 16);
+    tp = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(tp) + hfd::ent4_adv(e));
+    const uint32_t b = hfd::ent4_bits(e);
+    pos8 += b << 3;
+    npos -= b;
+    const uint32_t* rr = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(ring) + (pos8 & 0xF00u));
+    A = rr[0];
+    Bw = rr[64];
+  };
+
+  for (int blk = 0; blk < (int)(W / kBlk); blk++) {
+    blk_start(blk);
+    const uint32_t done = (uint32_t)blk * kBlk;
+    const uint32_t target = live && vlen > done ? min((uint32_t)kBlk, vlen - done) : 0u;
+    uint16_t* const tlim = dw.tile + lane * kTP4 + target;
+    auto quarter = [&]() {
+      if (tp < tlim && pos8 < rdy) {
+        uint32_t e = 0;
+#pragma unroll
+        for (int st = 0; st < kF; st++) {
+          e = tb.e[hfd::tab4_index(rg, __builtin_amdgcn_alignbit(A, Bw, npos))];
+          advance(e);
+        }
+        BPROF(pc[7] += __builtin_amdgcn_ballot_w64(e == 0) ? 1 : 0;)
+        if (__builtin_amdgcn_ballot_w64(e == 0)) {  // a code longer than 16 bits stopped the lane
+          if (e == 0) advance(hfd::lookup_long4(tb, rg, __builtin_amdgcn_alignbit(A, Bw, npos), dw.ubk));
+        }
+      }
+      BPROF(pc[6]++;)
+    };
+    // one group per two quarters (a lane reads at most 2 x 91 bits in them, 6 words: the ring
+    // buffers the difference), each in flight for four quarters
+    issue(pa, fa);
+    quarter();
+    quarter();
+    issue(pb, fb);
+    quarter();
+    quarter();
+    bool odd = false;
+    for (;;) {
+      consume(pa, fa);
+      issue(pa, fa);
+      quarter();
+      quarter();
+      BPROF(pc[5]++;)
+      if (!__builtin_amdgcn_ballot_w64(tp < tlim)) {
+        odd = true;
+        break;
+      }
+      consume(pb, fb);
+      issue(pb, fb);
+      quarter();
+      quarter();
+      BPROF(pc[5]++;)
+      if (!__builtin_amdgcn_ballot_w64(tp < tlim)) break;
+    }
+    BPROF(hfd::wave_sync(); tk = __builtin_readcyclecounter(); pc[2] += tk - tp0; tp0 = tk;)
+    if (odd) consume(pb, fb);  // drain in issue order: nothing stays in flight across the stores
+    consume(pa, fa);
+    consume(pb, fb);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a group no lane consumed may be in flight
+    hfd::wave_sync();
+    BPROF(tk = __builtin_readcyclecounter(); pc[3] += tk - tp0; tp0 = tk;)
+    // symbols decoded past the block end move to its front; they are held in registers across
+    // the reconstruction, which may use the tile as scratch
+    uint32_t* rw = reinterpret_cast<uint32_t*>(dw.tile + lane * kTP4);
+    uint32_t ovs[kF + 1];
+#pragma unroll
+    for (int i = 0; i <= kF; i++) ovs[i] = rw[kBlk / 2 + i];
+    recon(blk);
+    hfd::wave_sync();
+#pragma unroll
+    for (int i = 0; i <= kF; i++) rw[i] = ovs[i];
+    hfd::wave_sync();
+    // next block's columns; a lane that stopped short of the block (a dead or short chunk)
+    // restarts at column 0, where its (zero) target keeps it out of the quarters
+    uint16_t* const row = dw.tile + lane * kTP4;
+    tp = tp >= row + kBlk ? tp - kBlk : row;
+    BPROF(tk = __builtin_readcyclecounter(); pc[4] += tk - tp0; tp0 = tk;)
+  }
+}
+
 template <typename T, bool ZZ, bool BUF>
-__global__ void __launch_bounds__(64 * kDecWaves)
+__global__ void __launch_bounds__(64 * kDec4Waves)
 k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const uint8_t* __restrict__ revbook,
                 int bklen, const uint32_t* __restrict__ par_nbit, const uint32_t* __restrict__ par_entry, T* out,
                 uint32_t lx, uint32_t ly, uint32_t lz, T ebx2, T r, uint32_t nbx, uint32_t nby, uint32_t nbricks,
                 BrickOutliers ol)
 {
-  __shared__ hfd::LdsTables<kDecB> tb;  // static: table addresses fold into the ds offsets
+  __shared__ hfd::Tab4 tb;  // static: table addresses fold into the ds offsets
   extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
-  hfd::build_tables<kDecB>(tb, revbook, bklen);
-  const hfd::DecRegs rg = hfd::load_dec_regs(tb);
+  hfd::build_tab4(tb, revbook, bklen);
+  const hfd::DecRegs4 rg = hfd::load_dec_regs4(tb);
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* wbase = dsm + (size_t)wid * kDecWaveBytes;
-  uint16_t* tile = reinterpret_cast<uint16_t*>(wbase + kDecTile);
-  uint32_t* cval = reinterpret_cast<uint32_t*>(wbase + kDecCells);
-  BrickCells bc{cval, 1, reinterpret_cast<uint32_t*>(wbase + kDecRows), reinterpret_cast<uint32_t*>(wbase + kDecRows) + 65};
+  uint8_t* wbase = dsm + (size_t)wid * kD4WaveBytes;
+  uint16_t* tile = reinterpret_cast<uint16_t*>(wbase + kD4Tile);
+  uint32_t* cval = reinterpret_cast<uint32_t*>(wbase + kD4Cells);
+  BrickCells bc{cval, 1, reinterpret_cast<uint32_t*>(wbase + kD4Rows), reinterpret_cast<uint32_t*>(wbase + kD4Rows) + 65};
   const bool ranked = !ZZ && (ol.ncell == 0 || *ol.unsorted != ol.epoch);
-  const DecWave dw{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(bitstream), 0, (int)(bs_words * 4u), (int)kBufRsrcW3),
-                   reinterpret_cast<uint32_t*>(wbase) + lane, tile, (uint32_t)bklen, lane};
+  const DecWave4 dw{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(bitstream), 0, (int)(bs_words * 4u), (int)kBufRsrcW3),
+                    reinterpret_cast<uint32_t*>(wbase) + lane, tile, (uint32_t)bklen, lane};
   const size_t plane = (size_t)lx * ly;
   constexpr uint32_t W = 256;
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
@@ -1456,14 +1628,14 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
       const uint32_t nyv = min(8u, ly - y0), nzv = min(8u, lz - z0);
       const size_t base_elem = (size_t)z0 * plane + (size_t)y0 * lx + (size_t)bx * W + (size_t)blk * kBlk;
       if (ranked)
-        recon_block<T, ZZ, BUF, kTP, true>(tile, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane, &bc);
+        recon_block<T, ZZ, BUF, kTP4, true>(tile, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane, &bc);
       else
-        recon_block<T, ZZ, BUF, kTP, false>(tile, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane);
+        recon_block<T, ZZ, BUF, kTP4, false>(tile, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane);
     };
     auto blk_start = [&](int blk) {
       if (blk == (int)(W / kBlk) - 1) nx = fetch(brick + nw);
     };
-    decode_chunks(tb, rg, dw, live, vbase, nbit, W, pro, blk_start, recon BPROF_A, W, f2);
+    decode_chunks4(tb, rg, dw, live, vbase, nbit, W, pro, blk_start, recon BPROF_A4, W, f2);
   }
 #ifdef CUSZ_AMD_DEC_PROFILE
   if (lane == 0)
@@ -2393,9 +2565,9 @@ int launch_brick_decode(const BrickLaunch& L, const uint32_t* bitstream, size_t 
   const size_t plane = (size_t)L.lx * L.ly;
   const bool buf = (7 * plane + 7 * (size_t)L.lx + (size_t)kBlk) * sizeof(T) < (1ull << 31);
   const uint32_t bw = (uint32_t)bs_words;
-  const size_t lds = (size_t)kDecWaves * kDecWaveBytes;  // dynamic part
+  const size_t lds = (size_t)kDec4Waves * kD4WaveBytes;  // dynamic part
 #define DEC_LAUNCH(ZZ, BUF)                                                                                     \
-  k_brick3_decode<T, ZZ, BUF><<<L.ncu, 64 * kDecWaves, lds, st>>>(bitstream, bw, revbook, bklen, par_nbit, par_entry, \
+  k_brick3_decode<T, ZZ, BUF><<<L.ncu, 64 * kDec4Waves, lds, st>>>(bitstream, bw, revbook, bklen, par_nbit, par_entry, \
                                                                   out, L.lx, L.ly, L.lz, ebx2, r, g.nbx, g.nby,       \
                                                                   g.nbricks, ol)
   if (zz) {

@@ -313,5 +313,125 @@ __device__ __forceinline__ uint32_t lookup_l1_first(const LdsTables<B>& t, const
   return e;
 }
 
+// ---- compact decode tables (the 3-D fused decoder) ---------------------------------------------
+// One u32 entry per window, laid out for few instructions per decode step:
+//   [9:0] first symbol, [12:10] 2 x symbols (0, 2 or 4: the tile pointer's advance in bytes),
+//   [25:16] second symbol, [31:27] bits consumed; 0 = "no symbol, no bits" (a code longer than
+//   16 bits, or a window past the L2 cap: decoded by lookup_long).
+// L1 (2^12 entries) by the top 12 bits, one or two whole codewords; L2 (kL2Cap4 entries) right
+// after it, by the top 16 bits, for the windows below the canonical threshold first[12] << 20.
+// Stored symbols are (e & kEnt4SymMask): two u16 halves.
+constexpr int kL2Cap4 = 2048;
+constexpr uint32_t kEnt4SymMask = 0x03FF03FFu;
+__device__ __forceinline__ uint32_t ent4_pack(uint32_t nsym, uint32_t bits, uint32_t s0, uint32_t s1)
+{
+  return (bits << 27) | (s1 << 16) | ((2u * nsym) << 10) | s0;
+}
+__device__ __forceinline__ uint32_t ent4_bits(uint32_t e) { return e >> 27; }
+__device__ __forceinline__ uint32_t ent4_adv(uint32_t e) { return (e >> 10) & 7u; }
+
+struct Tab4 {
+  uint32_t e[(1 << 12) + kL2Cap4];
+  uint32_t first[32];
+  uint32_t base[32];
+  uint32_t entry[32];
+  uint32_t maxl;
+  uint16_t keys[kMaxBklen];
+};
+
+// Cooperative build by the whole workgroup (ends with a barrier); same decoding rule as
+// build_tables (hf_kernels.cuhip.inl:351-365), entries in the compact format.
+__device__ __forceinline__ void build_tab4(Tab4& t, const uint8_t* revbook, int bklen)
+{
+  constexpr int B = 12;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int32_t* rv = reinterpret_cast<const int32_t*>(revbook);
+  if (tid < 32) t.first[tid] = (uint32_t)rv[tid], t.entry[tid] = (uint32_t)rv[32 + tid];
+  const uint16_t* keys = reinterpret_cast<const uint16_t*>(revbook + 256);
+  for (int i = tid; i < bklen; i += nt) t.keys[i] = keys[i];
+  __syncthreads();
+  const int maxl = longest_code(t.entry);
+  if (tid < 32) {
+    t.base[tid] = t.entry[tid] - t.first[tid];
+    if (tid == 0) t.maxl = (uint32_t)maxl;
+  }
+  __syncthreads();
+  uint32_t first[32];
+#pragma unroll
+  for (int k = 0; k < 32; k++) first[k] = t.first[k];
+  const uint32_t ub = (uint32_t)bklen;
+  for (uint32_t i = tid; i < (1u << B); i += nt) {
+    const uint32_t v = i << (32 - B);
+    uint32_t s0, s1, e = 0;
+    const uint32_t l0 = tab_decode1(v, first, maxl, t.base, t.keys, ub, s0);
+    if (l0 <= (uint32_t)B) {
+      const uint32_t rest = B - l0;
+      const uint32_t l1 = rest ? tab_decode1(v << l0, first, maxl, t.base, t.keys, ub, s1) : 99u;
+      e = l1 <= rest ? ent4_pack(2, l0 + l1, s0, s1) : ent4_pack(1, l0, s0, 0);
+    }
+    t.e[i] = e;
+  }
+  const uint32_t P = maxl > B ? min(first[B], 1u << B) : 0u;
+  const uint32_t n2 = min(P << (kL2Bits - B), (uint32_t)kL2Cap4 - 1);
+  for (uint32_t q = tid; q < (uint32_t)kL2Cap4; q += nt) {
+    uint32_t e = 0;
+    if (q < n2) {
+      uint32_t s0;
+      const uint32_t l = tab_decode1(q << (32 - kL2Bits), first, maxl, t.base, t.keys, ub, s0);
+      if (l <= (uint32_t)kL2Bits) e = ent4_pack(1, l, s0, 0);
+    }
+    t.e[(1 << B) + q] = e;
+  }
+  __syncthreads();
+}
+
+// wave-uniform values for the compact decoder: the L1/L2 threshold and, for the rare codes no
+// table entry holds, the canonical thresholds of lengths 13..27 pre-shifted so that one compare
+// of (win >> 1) decides each: (win >> (32 - L)) < first[L]  <=>  (win >> 1) < first[L] << (31 - L)
+// (first[L] <= 2^L keeps the right side in 32 bits; lengths past the longest code never count).
+struct DecRegs4 {
+  uint32_t T[kLmax - 12];
+  uint32_t maxl;
+  uint32_t thr;
+};
+
+__device__ __forceinline__ DecRegs4 load_dec_regs4(const Tab4& t)
+{
+  constexpr int B = 12;
+  DecRegs4 r;
+  r.maxl = __builtin_amdgcn_readfirstlane(t.maxl);
+#pragma unroll
+  for (int q = 0; q < kLmax - 12; q++) {
+    const int L = 13 + q;
+    const uint32_t f = t.first[L];
+    const uint32_t v = L >= (int)t.maxl ? 0u : (f >= (1u << L) ? 0xFFFFFFFFu : f << (31 - L));
+    r.T[q] = __builtin_amdgcn_readfirstlane(v);
+  }
+  const uint32_t fb = __builtin_amdgcn_readfirstlane(t.first[B]);
+  r.thr = r.maxl <= (uint32_t)B ? 0u : (fb >= (1u << B) ? 0xFFFFFFFFu : fb << (32 - B));
+  return r;
+}
+
+// Index in Tab4::e of the entry for the codeword(s) at the top of `win` (L1 or L2 by the
+// canonical threshold: exclusive, one table read).
+__device__ __forceinline__ uint32_t tab4_index(const DecRegs4& rg, uint32_t win)
+{
+  return win < rg.thr ? (1u << 12) + min(win >> (32 - kL2Bits), (uint32_t)kL2Cap4 - 1) : win >> 20;
+}
+
+// Codes longer than 16 bits (and windows past the L2 cap): the length by counting the failing
+// lengths 13..27 (the reference rule, hf_kernels.cuhip.inl:351-365), one compare each; the
+// entry in the compact format (one symbol).
+__device__ __forceinline__ uint32_t lookup_long4(const Tab4& t, const DecRegs4& rg, uint32_t win, uint32_t bklen)
+{
+  const uint32_t h = win >> 1;
+  uint32_t l = 13;
+#pragma unroll
+  for (int q = 0; q < kLmax - 12; q++) l += h < rg.T[q] ? 1u : 0u;
+  if (l > rg.maxl) l = rg.maxl;
+  const uint32_t s = t.keys[min(t.base[l] + (win >> (32 - l)), bklen - 1)];
+  return ent4_pack(1, l, s, 0);
+}
+
 }  // namespace hfd
 }  // namespace cusz_amd

@@ -40,7 +40,7 @@ print(f"decompress {ev[0].elapsed_time(ev[1]) / reps * 1e3:.1f} us per call (pro
 for i, nm in [(1, "start"), (2, "decode"), (3, "drain"), (4, "recon")]:
     print(f"  {nm:7s} {v[i] / nbk:10.0f} cycles/brick")
 print(f"  loop iterations {v[5] / nbk:.1f}/brick ({v[5] / nbk * 2 * 4:.0f} wave-steps, kF = 4)")
-print(f"  lane-steps: done {v[7] / nbk:.0f}/brick, starved {v[6] / nbk:.0f}/brick")
+print(f"  3-D: quarters {v[6] / nbk:.1f}/brick, with a long code {v[7] / nbk:.1f}/brick; 1-D lane-steps: done {v[7] / nbk:.0f}/brick, starved {v[6] / nbk:.0f}/brick")
 if v[10]:
     print(f"  3-D ring refill waits {v[10] / nbk:.0f} cycles/brick")
 if v[8] or v[9]:

@@ -1,0 +1,17 @@
+#!/bin/bash
+# PMC passes over the 3-D fused decoder of a library variant (diagnostic):
+#   scripts/pmc_dec3.sh <lib dir> [tag]
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+lib=$1; tag=${2:-dec3}
+mkdir -p gpurun_out/$tag
+i=0
+for ctr in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
+           "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
+           "GRBM_GUI_ACTIVE GRBM_COUNT"; do
+  i=$((i+1))
+  CUSZ_AMD_LIB=$lib/libcusz_amd.so timeout -s KILL 90 rocprofv3 --kernel-include-regex "k_brick3_decode" --pmc $ctr -d gpurun_out/$tag/p$i -o run --output-format csv -- python3 scripts/brick_bench.py --reps 2 > gpurun_out/$tag/p$i.log 2>&1 || exit 1
+  python3 scripts/pmc_summary.py "$(find gpurun_out/$tag/p$i -name '*counter_collection.csv' | head -1)" > gpurun_out/$tag/p$i.summary
+  rm -rf gpurun_out/$tag/p$i
+done
+cat gpurun_out/$tag/p*.summary
