@@ -1012,61 +1012,102 @@ struct BrickCells {
   uint32_t* carry;       // LDS, 64 entries
 };
 
-// Reconstruct columns [xg0, xg0 + 64) of the brick from the code tile (lane = column, row pitch
-// TP).  lrz_x.cuhip.inl:271-360 order: v = (outlier + code) - r; y running sum (sequential); x then
-// z Hillis-Steele; times 2 eb.  Outlier values (code 0) come from the ranked cells (CELLS) or from
-// `out`, where the scatter pass has put them.
+// Column of the block a lane reconstructs.  Each 16-lane DPP row holds two 8-wide x tiles
+// interleaved -- even lanes the first, odd lanes the second -- so the x Hillis-Steele step d reads
+// lane - 2 d (row_shr 2 d) and the lanes whose source lies in the previous tile read past the DPP
+// row, which returns 0: no selects (lrz_x.cuhip.inl:311-353 order d = 1, 2, 4; t + 0 == t).
+__device__ __forceinline__ uint32_t rcol(uint32_t l) { return (l & 48u) | ((l & 1u) << 3) | ((l & 15u) >> 1); }
+
+template <int CTRL>
+__device__ __forceinline__ float dpp0(float v)
+{
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp0(double v)
+{
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, (unsigned long long)(uint32_t)lo | ((unsigned long long)(uint32_t)hi << 32));
+}
+template <typename T>
+__device__ __forceinline__ T x_scan8i(T t)
+{
+  t = t + dpp0<0x112>(t);  // row_shr:2 = column x - 1
+  t = t + dpp0<0x114>(t);  // row_shr:4 = column x - 2
+  t = t + dpp0<0x118>(t);  // row_shr:8 = column x - 4
+  return t;
+}
+
+// Rank, in column order, of this lane's zero code among the row's zero codes (m: ballot of the
+// row's zero codes over lanes; rcol's order: DPP rows in turn, even lanes before odd lanes).
+__device__ __forceinline__ uint32_t col_rank(uint64_t m, uint32_t l)
+{
+  const uint32_t r0 = l & 48u;
+  const uint32_t below = (uint32_t)__builtin_popcountll(m & ((1ull << r0) - 1ull));
+  const uint32_t row = (uint32_t)(m >> r0) & 0xFFFFu, li = l & 15u;
+  const uint32_t before = (1u << li) - 1u;
+  return below + ((l & 1u) ? (uint32_t)__builtin_popcount(row & 0x5555u) + (uint32_t)__builtin_popcount(row & 0xAAAAu & before)
+                           : (uint32_t)__builtin_popcount(row & 0x5555u & before));
+}
+
+// Reconstruct columns [x0, x0 + 64) of the brick from the code tile (lane l = column rcol(l),
+// row pitch TP).  lrz_x.cuhip.inl:271-360 order: v = (outlier + code) - r; y running sum
+// (sequential); x then z Hillis-Steele; times 2 eb.  Outlier values (code 0) come from the ranked
+// cells (CELLS) or from `out`, where the scatter pass has put them.  Stores address the block's
+// row (y, z) as a buffer at base + y lx with z plane as the scalar offset.
 template <typename T, bool ZZ, bool BUF, int TP, bool CELLS>
 __device__ __forceinline__ void recon_block(const uint16_t* tile, T* out, size_t plane, uint32_t lx, uint32_t nyv,
                                             uint32_t nzv, size_t base_elem, T r, T ebx2, int lane,
                                             const BrickCells* bc = nullptr)
 {
   T* base = out + base_elem;  // element (x0, y0, z0) of this block
-  const __amdgpu_buffer_rsrc_t ro = rsrc(base);
-  const uint32_t voff = (uint32_t)lane * sizeof(T);
-  const uint32_t l7 = (uint32_t)lane & 7u;
+  const uint32_t col = rcol((uint32_t)lane);
+  const uint32_t voff = col * (uint32_t)sizeof(T);
+  const bool full = nyv == 8u && nzv == 8u;  // wave-uniform
   T s[8];
 #pragma unroll
   for (int y = 0; y < 8; y++) {
     if ((uint32_t)y >= nyv) break;
     uint32_t cd[8];
 #pragma unroll
-    for (int z = 0; z < 8; z++) cd[z] = tile[(y * 8 + z) * TP + lane];
+    for (int z = 0; z < 8; z++) cd[z] = tile[(y * 8 + z) * TP + col];
     T v[8];
-    bool anyz = false;
 #pragma unroll
     for (int z = 0; z < 8; z++) {
       if constexpr (ZZ)
         v[z] = (T)zz_dec((uint16_t)cd[z]);
       else
         v[z] = (T)cd[z] - r;
-      anyz |= cd[z] == 0u;
     }
-    if (CELLS && __builtin_amdgcn_ballot_w64(anyz)) {  // outliers: ranked cells of the brick
+    const uint32_t mn = min(min(min(cd[0], cd[1]), min(cd[2], cd[3])), min(min(cd[4], cd[5]), min(cd[6], cd[7])));
+    if (__builtin_amdgcn_ballot_w64(mn == 0u)) {  // a zero code in this y step (rare)
+      if constexpr (CELLS) {  // outliers: ranked cells of the brick
 #pragma unroll
-      for (int z = 0; z < 8; z++) {
-        const uint64_t m = __builtin_amdgcn_ballot_w64(cd[z] == 0u);
-        if (m && (uint32_t)z < nzv) {
-          const uint32_t row = (uint32_t)y * 8u + (uint32_t)z;
-          const uint32_t c0 = bc->row_start[row] + bc->carry[row], ce = bc->row_start[row + 1];
-          const uint32_t j = c0 + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
-          if (cd[z] == 0u) v[z] = (j < ce ? (T)__builtin_bit_cast(float, bc->val[j * bc->vstride]) : T(0)) - r;
-          hfd::wave_sync();
-          if (lane == 0) bc->carry[row] += (uint32_t)__builtin_popcountll(m);
+        for (int z = 0; z < 8; z++) {
+          const uint64_t m = __builtin_amdgcn_ballot_w64(cd[z] == 0u);
+          if (m && (uint32_t)z < nzv) {
+            const uint32_t row = (uint32_t)y * 8u + (uint32_t)z;
+            const uint32_t c0 = bc->row_start[row] + bc->carry[row], ce = bc->row_start[row + 1];
+            const uint32_t j = c0 + col_rank(m, (uint32_t)lane);
+            if (cd[z] == 0u) v[z] = (j < ce ? (T)__builtin_bit_cast(float, bc->val[j * bc->vstride]) : T(0)) - r;
+            hfd::wave_sync();
+            if (lane == 0) bc->carry[row] += (uint32_t)__builtin_popcountll(m);
+          }
         }
       }
-    }
-    else if (!CELLS && __builtin_amdgcn_ballot_w64(anyz)) {  // outliers: their values were scattered into out
-      // every row with an outlier is loaded whole (uniform branch), then one wait for all
-      T ov[8];
+      else {  // outliers: their values were scattered into out
+        T ov[8];
 #pragma unroll
-      for (int z = 0; z < 8; z++) {
-        ov[z] = T(0);
-        if (__builtin_amdgcn_ballot_w64(cd[z] == 0u) && (uint32_t)z < nzv) ov[z] = base[(size_t)z * plane + (size_t)y * lx + lane];
+        for (int z = 0; z < 8; z++) {
+          ov[z] = T(0);
+          if (__builtin_amdgcn_ballot_w64(cd[z] == 0u) && (uint32_t)z < nzv) ov[z] = base[(size_t)z * plane + (size_t)y * lx + col];
+        }
+#pragma unroll
+        for (int z = 0; z < 8; z++)
+          if (cd[z] == 0u) v[z] = ZZ ? ov[z] + T(0) : ov[z] - r;
       }
-#pragma unroll
-      for (int z = 0; z < 8; z++)
-        if (cd[z] == 0u) v[z] = ZZ ? ov[z] + T(0) : ov[z] - r;
     }
     T t[8];
     if constexpr (sizeof(T) == 4) {
@@ -1079,7 +1120,7 @@ __device__ __forceinline__ void recon_block(const uint16_t* tile, T* out, size_t
         const f2 vv = {v[2 * j], v[2 * j + 1]};
         sv = y > 0 ? sv + vv : vv;
         s[2 * j] = sv.x, s[2 * j + 1] = sv.y;
-        t[2 * j] = x_scan8<T>(sv.x, l7), t[2 * j + 1] = x_scan8<T>(sv.y, l7);
+        t[2 * j] = x_scan8i<T>(sv.x), t[2 * j + 1] = x_scan8i<T>(sv.y);
       }
 #pragma unroll
       for (int z = 7; z >= 1; z--) t[z] = t[z] + t[z - 1];
@@ -1097,7 +1138,7 @@ __device__ __forceinline__ void recon_block(const uint16_t* tile, T* out, size_t
 #pragma unroll
       for (int z = 0; z < 8; z++) {
         s[z] = y > 0 ? s[z] + v[z] : v[z];
-        t[z] = x_scan8<T>(s[z], l7);
+        t[z] = x_scan8i<T>(s[z]);
       }
 #pragma unroll
       for (int d = 1; d < 8; d *= 2)
@@ -1106,17 +1147,23 @@ __device__ __forceinline__ void recon_block(const uint16_t* tile, T* out, size_t
 #pragma unroll
       for (int z = 0; z < 8; z++) t[z] = t[z] * ebx2;
     }
+    T* rowb = base + (size_t)y * lx;
+    if constexpr (BUF) {
+      const __amdgpu_buffer_rsrc_t ro = rsrc(rowb);
+      if (full) {
 #pragma unroll
-    for (int z = 0; z < 8; z++) {
-      if ((uint32_t)z >= nzv) break;
-      const T o = t[z];
-#ifdef CUSZ_AMD_EXP_NOSTORE
-      if (true) { asm volatile("" ::"v"(o)); continue; }
-#endif
-      if constexpr (BUF)
-        buf_store<T>(o, ro, voff, (uint32_t)(((size_t)z * plane + (size_t)y * lx) * sizeof(T)));
-      else
-        base[(size_t)z * plane + (size_t)y * lx + lane] = o;
+        for (int z = 0; z < 8; z++) buf_store<T>(t[z], ro, voff, (uint32_t)((size_t)z * plane * sizeof(T)));
+      }
+      else {
+#pragma unroll
+        for (int z = 0; z < 8; z++)
+          if ((uint32_t)z < nzv) buf_store<T>(t[z], ro, voff, (uint32_t)((size_t)z * plane * sizeof(T)));
+      }
+    }
+    else {
+#pragma unroll
+      for (int z = 0; z < 8; z++)
+        if ((uint32_t)z < nzv) rowb[(size_t)z * plane + col] = t[z];
     }
   }
 }
