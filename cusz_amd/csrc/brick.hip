@@ -1430,8 +1430,15 @@ constexpr size_t kD4WaveBytes = kD4Rows + (size_t)(65 + 64) * 4;
 #ifndef CUSZ_AMD_DEC4_WAVES
 #define CUSZ_AMD_DEC4_WAVES 9
 #endif
+#ifndef CUSZ_AMD_DEC4_REGWIN
+#define CUSZ_AMD_DEC4_REGWIN 0
+#endif
 constexpr int kDec4Waves = CUSZ_AMD_DEC4_WAVES;
 static_assert(sizeof(hfd::Tab4) + kDec4Waves * kD4WaveBytes <= 160 * 1024, "LDS");
+
+// pos8 limit for entering a quarter: every word the quarter reads (<= 4 x 16 + 27 bits on) is in
+// the ring (window pair: p + 122 < 32 ctop; register window, which reads word J + 3: p + 186)
+constexpr uint32_t kRdy4 = CUSZ_AMD_DEC4_REGWIN ? 8u * (511u - 186u) : 8u * (511u - 123u);
 
 struct DecWave4 {
   __amdgpu_buffer_rsrc_t rbits;
@@ -1458,12 +1465,18 @@ __device__ __forceinline__ void decode_chunks4(const hfd::Tab4& tb, const hfd::D
   ring[0] = a0.x, ring[64] = a0.y, ring[2 * 64] = a0.z, ring[3 * 64] = a0.w;
   ring[4 * 64] = a1.x, ring[5 * 64] = a1.y, ring[6 * 64] = a1.z, ring[7 * 64] = a1.w;
   ring[16 * 64] = a0.x;  // mirror of slot 0
+#if CUSZ_AMD_DEC4_REGWIN
+  // (variant) window in registers: w0:w1 the 64-bit window, w2 and nx the next words (nx = word
+  // kk, re-read from the ring every step), sh = 32 - bits of w0 consumed
+  uint32_t w0 = 0, w1 = a0.x, w2 = a0.y, nx = a0.z, sh = 0, kk = 2;
+#else
   uint32_t A = 0, Bw = a0.x;  // words J, J + 1 of the window (J = -1 at bit 0: junk, shift 0)
+#endif
   uint32_t pos8 = 8u * 511u, npos = 0;  // 8 x (chunk bit position + 511); -position (the shift)
   uint32_t ltop = 8, ctop = 8;   // words requested / written to the ring
   // a quarter reaches at most 4 x 16 + 27 bits: the lane steps only if their words are in
   // (pos8 < 8 (32 ctop + 388))
-  uint32_t rdy = ctop >= nwords ? 0xFFFFFFFFu : 256u * ctop + 8u * 388u;
+  uint32_t rdy = ctop >= nwords ? 0xFFFFFFFFu : 256u * ctop + kRdy4;
   uint16_t* tp = dw.tile + lane * kTP4;
   u32x4 pa, pb;  // groups in flight
   bool fa = false, fb = false;
@@ -1483,7 +1496,7 @@ __device__ __forceinline__ void decode_chunks4(const hfd::Tab4& tb, const hfd::D
       sl[0] = p.x, sl[64] = p.y, sl[128] = p.z, sl[192] = p.w;
       if ((ctop & (kRing4 - 1u)) == 0u) ring[16 * 64] = p.x;
       ctop += 4u;
-      rdy = ctop >= nwords ? 0xFFFFFFFFu : 256u * ctop + 8u * 388u;
+      rdy = ctop >= nwords ? 0xFFFFFFFFu : 256u * ctop + kRdy4;
     }
     f = false;
   };
@@ -1495,12 +1508,29 @@ __device__ __forceinline__ void decode_chunks4(const hfd::Tab4& tb, const hfd::D
     tp[1] = (uint16_t)(sy >> 16);
     tp = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(tp) + hfd::ent4_adv(e));
     const uint32_t b = hfd::ent4_bits(e);
+#if CUSZ_AMD_DEC4_REGWIN
+    const int32_t s2 = (int32_t)sh - (int32_t)b;
+    const bool shf = s2 < 0;  // crossed into the next word
+    sh = (uint32_t)s2 & 31u;
+    w0 = shf ? w1 : w0;
+    w1 = shf ? w2 : w1;
+    w2 = shf ? nx : w2;
+    kk += shf ? 1u : 0u;
+    nx = ring[(kk & (kRing4 - 1u)) * 64];
+    pos8 += b << 3;
+#else
     pos8 += b << 3;
     npos -= b;
     const uint32_t* rr = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(ring) + (pos8 & 0xF00u));
     A = rr[0];
     Bw = rr[64];
+#endif
   };
+#if CUSZ_AMD_DEC4_REGWIN
+  auto window = [&]() { return __builtin_amdgcn_alignbit(w0, w1, sh); };
+#else
+  auto window = [&]() { return __builtin_amdgcn_alignbit(A, Bw, npos); };
+#endif
 
   for (int blk = 0; blk < (int)(W / kBlk); blk++) {
     blk_start(blk);
@@ -1508,16 +1538,18 @@ __device__ __forceinline__ void decode_chunks4(const hfd::Tab4& tb, const hfd::D
     const uint32_t target = live && vlen > done ? min((uint32_t)kBlk, vlen - done) : 0u;
     uint16_t* const tlim = dw.tile + lane * kTP4 + target;
     auto quarter = [&]() {
+      BPROF(pc[8] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(tp < tlim && !(pos8 < rdy)));
+            pc[9] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(tp < tlim));)
       if (tp < tlim && pos8 < rdy) {
         uint32_t e = 0;
 #pragma unroll
         for (int st = 0; st < kF; st++) {
-          e = tb.e[hfd::tab4_index(rg, __builtin_amdgcn_alignbit(A, Bw, npos))];
+          e = tb.e[hfd::tab4_index(rg, window())];
           advance(e);
         }
         BPROF(pc[7] += __builtin_amdgcn_ballot_w64(e == 0) ? 1 : 0;)
         if (__builtin_amdgcn_ballot_w64(e == 0)) {  // a code longer than 16 bits stopped the lane
-          if (e == 0) advance(hfd::lookup_long4(tb, rg, __builtin_amdgcn_alignbit(A, Bw, npos), dw.ubk));
+          if (e == 0) advance(hfd::lookup_long4(tb, rg, window(), dw.ubk));
         }
       }
       BPROF(pc[6]++;)
@@ -1531,12 +1563,17 @@ __device__ __forceinline__ void decode_chunks4(const hfd::Tab4& tb, const hfd::D
     quarter();
     quarter();
     bool odd = false;
+    // the block ends after the first quarter that leaves no lane short of it
     for (;;) {
       consume(pa, fa);
       issue(pa, fa);
       quarter();
-      quarter();
       BPROF(pc[5]++;)
+      if (!__builtin_amdgcn_ballot_w64(tp < tlim)) {
+        odd = true;
+        break;
+      }
+      quarter();
       if (!__builtin_amdgcn_ballot_w64(tp < tlim)) {
         odd = true;
         break;
@@ -1544,8 +1581,9 @@ __device__ __forceinline__ void decode_chunks4(const hfd::Tab4& tb, const hfd::D
       consume(pb, fb);
       issue(pb, fb);
       quarter();
-      quarter();
       BPROF(pc[5]++;)
+      if (!__builtin_amdgcn_ballot_w64(tp < tlim)) break;
+      quarter();
       if (!__builtin_amdgcn_ballot_w64(tp < tlim)) break;
     }
     BPROF(hfd::wave_sync(); tk = __builtin_readcyclecounter(); pc[2] += tk - tp0; tp0 = tk;)

@@ -332,6 +332,7 @@ __device__ __forceinline__ uint32_t ent4_adv(uint32_t e) { return (e >> 10) & 7u
 
 struct Tab4 {
   uint32_t e[(1 << 12) + kL2Cap4];
+  uint32_t T[16];  // lookup_long4's thresholds, lengths 13..27 (load_dec_regs4)
   uint32_t first[32];
   uint32_t base[32];
   uint32_t entry[32];
@@ -385,30 +386,30 @@ __device__ __forceinline__ void build_tab4(Tab4& t, const uint8_t* revbook, int 
   __syncthreads();
 }
 
-// wave-uniform values for the compact decoder: the L1/L2 threshold and, for the rare codes no
-// table entry holds, the canonical thresholds of lengths 13..27 pre-shifted so that one compare
-// of (win >> 1) decides each: (win >> (32 - L)) < first[L]  <=>  (win >> 1) < first[L] << (31 - L)
+// Wave-uniform values for the compact decoder: the L1/L2 threshold and the longest code; and in
+// Tab4::T, for the rare codes no table entry holds, the canonical thresholds of lengths 13..27
+// pre-shifted so that one compare of (win >> 1) decides each:
+//   (win >> (32 - L)) < first[L]  <=>  (win >> 1) < first[L] << (31 - L)
 // (first[L] <= 2^L keeps the right side in 32 bits; lengths past the longest code never count).
 struct DecRegs4 {
-  uint32_t T[kLmax - 12];
   uint32_t maxl;
   uint32_t thr;
 };
 
-__device__ __forceinline__ DecRegs4 load_dec_regs4(const Tab4& t)
+// Called by every thread after build_tab4 (ends with a barrier: thread q < 15 writes T[q]).
+__device__ __forceinline__ DecRegs4 load_dec_regs4(Tab4& t)
 {
   constexpr int B = 12;
   DecRegs4 r;
   r.maxl = __builtin_amdgcn_readfirstlane(t.maxl);
-#pragma unroll
-  for (int q = 0; q < kLmax - 12; q++) {
-    const int L = 13 + q;
-    const uint32_t f = t.first[L];
-    const uint32_t v = L >= (int)t.maxl ? 0u : (f >= (1u << L) ? 0xFFFFFFFFu : f << (31 - L));
-    r.T[q] = __builtin_amdgcn_readfirstlane(v);
+  if (threadIdx.x < 16) {
+    const int L = 13 + (int)threadIdx.x;
+    const uint32_t f = L <= kLmax ? t.first[L] : 0u;
+    t.T[threadIdx.x] = L > kLmax || L >= (int)r.maxl ? 0u : (f >= (1u << L) ? 0xFFFFFFFFu : f << (31 - L));
   }
   const uint32_t fb = __builtin_amdgcn_readfirstlane(t.first[B]);
   r.thr = r.maxl <= (uint32_t)B ? 0u : (fb >= (1u << B) ? 0xFFFFFFFFu : fb << (32 - B));
+  __syncthreads();
   return r;
 }
 
@@ -426,8 +427,10 @@ __device__ __forceinline__ uint32_t lookup_long4(const Tab4& t, const DecRegs4& 
 {
   const uint32_t h = win >> 1;
   uint32_t l = 13;
+  uint32_t T[16];
+  __builtin_memcpy(T, t.T, sizeof(T));  // wave-uniform: broadcast LDS reads (keeps SGPRs free)
 #pragma unroll
-  for (int q = 0; q < kLmax - 12; q++) l += h < rg.T[q] ? 1u : 0u;
+  for (int q = 0; q < kLmax - 12; q++) l += h < T[q] ? 1u : 0u;
   if (l > rg.maxl) l = rg.maxl;
   const uint32_t s = t.keys[min(t.base[l] + (win >> (32 - l)), bklen - 1)];
   return ent4_pack(1, l, s, 0);

@@ -43,6 +43,8 @@ print(f"  loop iterations {v[5] / nbk:.1f}/brick ({v[5] / nbk * 2 * 4:.0f} wave-
 print(f"  3-D: quarters {v[6] / nbk:.1f}/brick, with a long code {v[7] / nbk:.1f}/brick; 1-D lane-steps: done {v[7] / nbk:.0f}/brick, starved {v[6] / nbk:.0f}/brick")
 if v[10]:
     print(f"  3-D ring refill waits {v[10] / nbk:.0f} cycles/brick")
-if v[8] or v[9]:
+if v[9] and not v[10]:
+    print(f"  3-D lane-quarters: wanting {v[9] / nbk:.0f}/brick, starved {v[8] / nbk:.0f}/brick")
+elif v[8] or v[9]:
     print(f"  1-D recon: values {v[8] / nbk:.0f}, scans + stores {v[9] / nbk:.0f} cycles/brick")
 print(f"max err {(y.double() - x.double()).abs().max().item():.3e}")
