@@ -60,6 +60,10 @@ def parse():
                          "gather to root); 5 = 512^3 f64 cuSZ-i spline, r2r 1e-6")
     ap.add_argument("--dims", default=None)
     ap.add_argument("--eb", type=float, default=None)
+    ap.add_argument("--rotate", type=int, default=3,
+                    help="distinct input fields the timed loop cycles through (different seeds), so that no "
+                         "step reads an input the previous steps left in the 256 MiB Infinity Cache; "
+                         "the same-field rate is reported beside it")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (PCIe) path timing")
     ap.add_argument("--profile-only", action="store_true", help="few steps, no baselines (rocprof)")
@@ -199,15 +203,25 @@ def bench_field(args, world, rank, dist, dev):
     my_dims, n = slab.dims, slab.count
     seed = {1: 1, 2: 2, 3: 3, 5: 5}[args.config] + (rank if weak else 0)
 
-    if args.config == 1:
-        d_full = torch.from_numpy(datagen.cesm2d_np(dims[:2], seed=seed)).to(dev)
-    elif args.config == 3:
-        d_full = datagen.hacc1d_torch(n_full, seed=seed, device=dev)
-    else:
-        d_full = datagen.smooth3d_torch(dims, seed=seed, dtype=tdt, device=dev)
+    def make_field(sd):
+        if args.config == 1:
+            return torch.from_numpy(datagen.cesm2d_np(dims[:2], seed=sd)).to(dev)
+        if args.config == 3:
+            return datagen.hacc1d_torch(n_full, seed=sd, device=dev)
+        return datagen.smooth3d_torch(dims, seed=sd, dtype=tdt, device=dev)
+
+    d_full = make_field(seed)
     d_in = d_full[slab.offset:slab.offset + n].clone() if sharded else d_full
     if sharded and rank != 0:
         del d_full  # the root keeps the whole field to validate the merged archive
+    # the timed loop cycles through `rotate` fields of the same recipe (other seeds): a step never
+    # reads an input that earlier steps left in the Infinity Cache
+    inputs = [d_in]
+    for k in range(1, max(1, args.rotate)):
+        f = make_field(seed + 1000 * k)
+        inputs.append(f[slab.offset:slab.offset + n].clone() if sharded else f)
+        del f
+    cur = {"i": 0}
     d_out = torch.empty(n, dtype=tdt, device=dev)
     stream = torch.cuda.current_stream(dev)
     r = cz.Resource(cz.F4 if esz == 4 else cz.F8, my_dims, predictor, stream=stream.cuda_stream)
@@ -218,18 +232,21 @@ def bench_field(args, world, rank, dist, dev):
     state = {"scratch": None, "parts": None}
 
     def compress():
+        x = inputs[cur["i"]]
         if not sharded:
-            ptr, nb, _ = r.compress(d_in.data_ptr(), args.eb, mode)
+            ptr, nb, _ = r.compress(x.data_ptr(), args.eb, mode)
             return ptr, nb
         eb = args.eb
         if mode == cz.Rel:  # r2r: eb times the whole field's value range (one all-reduce)
-            eb *= shard.global_value_ranges([r], [d_in], dist)[0]
-        r.compress_scan(d_in.data_ptr(), eb, hist.data_ptr())
+            eb *= shard.global_value_ranges([r], [x], dist)[0]
+        r.compress_scan(x.data_ptr(), eb, hist.data_ptr())
         shard.allreduce_histograms(hist, dist)  # RCCL, ordered on this stream: no host sync
         ptr, nb, _ = r.compress_finish(hist.data_ptr())
         return ptr, nb
 
-    def step(acc=None):
+    def step(acc=None, rot=True):
+        if acc is not None:  # phase split: nothing of the previous step is still queued
+            torch.cuda.synchronize()
         t0 = time.perf_counter()
         ptr, nb = compress()  # host-synchronous (the archive header is read back)
         t1 = time.perf_counter()
@@ -239,8 +256,12 @@ def bench_field(args, world, rank, dist, dev):
         t2 = time.perf_counter()
         r.decompress(ptr, nb, d_out.data_ptr())
         if acc is not None:
+            torch.cuda.synchronize()
             acc[0] += t1 - t0
             acc[1] += t2 - t1
+            acc[2] += time.perf_counter() - t2
+        if rot:
+            cur["i"] = (cur["i"] + 1) % len(inputs)
         return ptr, nb
 
     def barrier():
@@ -248,31 +269,42 @@ def bench_field(args, world, rank, dist, dev):
             dist.barrier()
 
     r.enable_timing(False)
-    for _ in range(args.warmup):
+    err = 0.0
+    for w in range(max(args.warmup, len(inputs))):
+        x = inputs[cur["i"]]
         step()
-    torch.cuda.synchronize()
-
-    # correctness guard on the measured configuration (error bound, every element)
-    err = (d_out.double() - d_in.double()).abs().max().item()
+        torch.cuda.synchronize()
+        # correctness guard on the measured configuration (error bound, every element, every field)
+        err = max(err, (d_out.double() - x.double()).abs().max().item())
+    cur["i"] = 0
     eb_abs = r.header.rc.eb  # Rel mode: eb * value range
     # the reconstruction is computed in T (lrz_x.cuhip.inl / spline3.inl), so T's rounding at the
     # field's magnitude adds to the bound (f32 at |x| ~ 256, HACC-like config 3: ~8e-6)
-    ulp = (2.0 ** -23 if esz == 4 else 2.0 ** -52) * d_in.abs().max().item()
+    ulp = (2.0 ** -23 if esz == 4 else 2.0 ** -52) * max(x.abs().max().item() for x in inputs)
     assert err <= 1.001 * eb_abs + ulp, f"error bound violated: {err} > {eb_abs} (+ulp {ulp})"
 
     # timed region: the library's HIP-event stage timing is OFF (its event records would add
     # barrier packets to the stream); the per-stage/kernel durations come from a second pass.
     # Decompress is asynchronous: step i's decompress overlaps the host side of step i+1's
     # compress on the same stream (nothing is skipped: every step's kernels run in order).
-    acc = [0.0, 0.0]
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    def timed(rot):
+        cur["i"] = 0
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step(rot=rot)
+        torch.cuda.synchronize()
+        barrier()
+        return time.perf_counter() - t0
+
+    dt_same = timed(False)  # every step on the same field (its input may stay cached)
+    dt = timed(True)        # `value`: the steps cycle through the distinct fields
+    # host-clock phase split (a separate pass: each step starts and ends with an idle stream)
+    acc = [0.0, 0.0, 0.0]
     for _ in range(args.steps):
-        ptr, nb = step(acc)
-    torch.cuda.synchronize()
-    barrier()
-    dt = time.perf_counter() - t0
+        step(acc)
+    cur["i"] = 0
     # same steps again with stage timing on (HIP events on the manager's stream)
     r.enable_timing(True)
     stage_acc = np.zeros(cz.T_COUNT)
@@ -281,12 +313,13 @@ def bench_field(args, world, rank, dist, dev):
         torch.cuda.synchronize()
         stage_acc += np.array(r.stage_times())
     r.enable_timing(False)
-    ptr, nb = step()
+    cur["i"] = 0
+    ptr, nb = step(rot=False)  # field 0's archive for what follows (CR, merge, roofline)
     torch.cuda.synchronize()
     if dist is not None:
-        t = torch.tensor([dt, acc[0], acc[1], err / max(eb_abs, 1e-300)], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt, dt_same, acc[0], acc[1], acc[2]], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt, acc[0], acc[1], rel_err = t.tolist()
+        dt, dt_same, acc[0], acc[1], acc[2] = t.tolist()
     ms_per_step = 1e3 * dt / args.steps
     value = total_bytes * args.steps / dt / 1e9
     st = stage_acc / args.steps
@@ -370,25 +403,24 @@ def bench_field(args, world, rank, dist, dev):
     sampled = None
     if world == 1 and ino.layout == cz.LAYOUT_BRICK and dims[1] > 1 and dims[2] > 1 and predictor != cz.Spline:
         r.set_codebook(cz.CODEBOOK_SAMPLED)
+        cur["i"] = 0
         for _ in range(args.warmup):
-            step()
+            step(rot=False)
         torch.cuda.synchronize()
         e_s = (d_out.double() - d_in.double()).abs().max().item()
-        t1 = time.perf_counter()
-        for _ in range(args.steps):
-            ptr_s, nb_s = step()
-        torch.cuda.synchronize()
-        dt_s = time.perf_counter() - t1
+        ptr_s, nb_s = step(rot=False)
+        dt_s = timed(True)
         r.enable_timing(True)
         st_s = np.zeros(cz.T_COUNT)
         for _ in range(args.steps):
-            ptr_s, nb_s = step()
+            step()
             torch.cuda.synchronize()
             st_s += np.array(r.stage_times())
         r.enable_timing(False)
         st_s /= args.steps
         r.set_codebook(cz.CODEBOOK_EXACT)
-        ptr, nb = step()  # the exact archive again for what follows
+        cur["i"] = 0
+        ptr, nb = step(rot=False)  # the exact archive again for what follows
         torch.cuda.synchronize()
         c_ms = st_s[cz.T_COMPRESS]
         sampled = {"value": round(total_bytes * args.steps / dt_s / 1e9, 2),
@@ -434,6 +466,7 @@ def bench_field(args, world, rank, dist, dev):
     if rank == 0:
         tg_ms = 1e3 * acc[1] / args.steps
         tc_ms = 1e3 * acc[0] / args.steps
+        td_ms = 1e3 * acc[2] / args.steps
         line = {
             "metric": METRICS[args.config],
             # only config 2 is BASELINE.json's metric workload; the others use the same fields
@@ -460,9 +493,13 @@ def bench_field(args, world, rank, dist, dev):
             "decompress_gbps": round(nbytes_in / (decomp_ms * 1e-3) / 1e9, 2) if decomp_ms > 0 else None,
             "compress_roofline_frac": round(nbytes_in / (comp_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if comp_ms > 0 else None,
             "decompress_roofline_frac": round(nbytes_in / (decomp_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if decomp_ms > 0 else None,
-            "phases_ms": {"compress": round(tc_ms, 4), "gather": round(tg_ms, 4),
-                          "decompress_and_rest": round(ms_per_step - tc_ms - tg_ms, 4)},
-            "field_compress_gbps": round(total_bytes / (tc_ms * 1e-3) / 1e9, 2) if tc_ms > 0 else None,
+            "rotating_inputs": len(inputs),
+            "same_field_value": round(total_bytes * args.steps / dt_same / 1e9, 2),
+            "same_field_ms_per_step": round(1e3 * dt_same / args.steps, 4),
+            # host clock, a separate pass in which every step starts and ends on an idle stream
+            "host_phases_ms": {"compress_call": round(tc_ms, 4), "gather": round(tg_ms, 4),
+                               "decompress_to_idle": round(td_ms, 4)},
+            "field_compress_call_gbps": round(total_bytes / (tc_ms * 1e-3) / 1e9, 2) if tc_ms > 0 else None,
             "field_compress_gather_gbps": round(total_bytes / ((tc_ms + tg_ms) * 1e-3) / 1e9, 2) if tc_ms > 0 else None,
             "compression_ratio": round(ratio, 3),
             "stages_ms": {k: round(float(st[i]), 4) for k, i in
