@@ -1460,7 +1460,13 @@ __device__ __forceinline__ void decode_chunks4(const hfd::Tab4& tb, const hfd::D
   const int lane = dw.lane;
   uint32_t* const ring = dw.ring_lane;
   const uint32_t nwords = live ? (nbit + 31u) >> 5 : 0u;
-  const u32x4 a0 = first[0], a1 = first[1];
+  u32x4 a0, a1;  // words 0..7: loaded by the caller ahead of time (first[0..1]), or now
+  if (first)
+    a0 = first[0], a1 = first[1];
+  else {
+    a0 = __builtin_amdgcn_raw_buffer_load_b128(dw.rbits, (int)(live ? vbase : kOOB), 0, 0);
+    a1 = __builtin_amdgcn_raw_buffer_load_b128(dw.rbits, (int)(live ? vbase + 16u : kOOB), 0, 0);
+  }
   pro();
   ring[0] = a0.x, ring[64] = a0.y, ring[2 * 64] = a0.z, ring[3 * 64] = a0.w;
   ring[4 * 64] = a1.x, ring[5 * 64] = a1.y, ring[6 * 64] = a1.z, ring[7 * 64] = a1.w;
@@ -1743,11 +1749,11 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
 // the prefetch read the cell directly.
 constexpr uint32_t kCellPf = 8;
 constexpr uint32_t kCvPitch = kCellPf + 1;  // odd word pitch: lane rows on distinct banks
-constexpr size_t kD1Cv = kDecTile + (size_t)64 * kTP * 2;  // values[64][kCvPitch]
+constexpr size_t kD1Cv = kD4Tile + (size_t)64 * kTP4 * 2;  // values[64][kCvPitch]
 constexpr size_t kD1WaveBytes = kD1Cv + (size_t)64 * kCvPitch * 4;
-constexpr int kD1MaxWaves = (int)((160 * 1024 - sizeof(hfd::LdsTables<kDecB>) - 512) / kD1WaveBytes);
+constexpr int kD1MaxWaves = (int)((160 * 1024 - sizeof(hfd::Tab4) - 512) / kD1WaveBytes);
 static_assert(kD1MaxWaves >= 4, "LDS");
-static_assert(64 * 144 <= 64 * kTP * 2, "store staging fits the code tile");
+static_assert(64 * 144 <= 64 * kTP4 * 2, "store staging fits the code tile");
 
 template <typename T, bool ZZ>
 __global__ void __launch_bounds__(64 * kDecWaves)
@@ -1755,18 +1761,18 @@ k_brick1_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
                 int bklen, const uint32_t* __restrict__ par_nbit, const uint32_t* __restrict__ par_entry, T* out,
                 size_t n, T ebx2, T r, uint32_t nchunks, uint32_t nunits, BrickOutliers ol)
 {
-  __shared__ hfd::LdsTables<kDecB> tb;
+  __shared__ hfd::Tab4 tb;
   extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
-  hfd::build_tables<kDecB>(tb, revbook, bklen);
-  const hfd::DecRegs rg = hfd::load_dec_regs(tb);
+  hfd::build_tab4(tb, revbook, bklen);
+  const hfd::DecRegs4 rg = hfd::load_dec_regs4(tb);
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* wbase = dsm + (size_t)wid * kD1WaveBytes;
-  uint16_t* tile = reinterpret_cast<uint16_t*>(wbase + kDecTile);
+  uint16_t* tile = reinterpret_cast<uint16_t*>(wbase + kD4Tile);
   uint32_t* cv = reinterpret_cast<uint32_t*>(wbase + kD1Cv) + lane * kCvPitch;  // this lane's values
   const bool ranked = !ZZ && (ol.ncell == 0 || *ol.unsorted != ol.epoch);  // else: values in `out` (scatter)
   const uint32_t npf = ol.ncell < (1u << 28) ? kCellPf : 0u;  // prefetched ranks (32-bit buffer offsets)
-  const DecWave dw{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(bitstream), 0, (int)(bs_words * 4u), (int)kBufRsrcW3),
-                   reinterpret_cast<uint32_t*>(wbase) + lane, tile, (uint32_t)bklen, lane};
+  const DecWave4 dw{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(bitstream), 0, (int)(bs_words * 4u), (int)kBufRsrcW3),
+                    reinterpret_cast<uint32_t*>(wbase) + lane, tile, (uint32_t)bklen, lane};
   const __amdgpu_buffer_rsrc_t rcells = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint32_t*>(ol.cells), 0, (int)min(ol.ncell * 8, (size_t)0x7FFFFFFF), (int)kBufRsrcW3);
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
@@ -1819,7 +1825,7 @@ k_brick1_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
         if (blk < 100) return;
 #endif
         const uint32_t roff = ((uint32_t)lane * 1024u + p * 256u + (uint32_t)blk * kBlk) * (uint32_t)sizeof(T);
-        const uint32_t* trow = reinterpret_cast<const uint32_t*>(tile + lane * kTP);
+        const uint32_t* trow = reinterpret_cast<const uint32_t*>(tile + lane * kTP4);
         if (ranked) {  // the prefetched values; ranks at or past the chunk's last cell read 0
 #pragma unroll
           for (int h = 0; h < (int)kCellPf / 2; h++) {
@@ -2035,7 +2041,7 @@ k_brick1_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
         if (blk & 1) carry = carry + tot;
         BPROF(pc[9] += __builtin_readcyclecounter() - tv;)
       };
-      decode_chunks(tb, rg, dw, live, vbase, nbit, vlen, pro, blk_start, recon BPROF_A);
+      decode_chunks4(tb, rg, dw, live, vbase, nbit, vlen, pro, blk_start, recon BPROF_A4, 256, nullptr);
     }
   }
 #ifdef CUSZ_AMD_DEC_PROFILE

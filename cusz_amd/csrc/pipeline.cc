@@ -257,6 +257,20 @@ struct Pipeline {
     return PSZ_SUCCESS;
   }
 
+  // Outlier capacity beyond the reference's 10 % (buf_comp.cc:87-88, compressor.inl:368-372 fail
+  // the compress there): a spill list for `need` cells (bounded by n) and an archive to match.
+  // 1: grown, 0: already at the bound, -1: allocation failure.
+  int grow_spill(uint64_t need)
+  {
+    const uint64_t cap = std::min<uint64_t>(need + need / 8 + 1024, (uint64_t)n + 1024);
+    if (cap <= spill_cap) return 0;
+    (void)hipFree(d_spill);
+    d_spill = nullptr;
+    if (hipMalloc(&d_spill, cap * 8) != hipSuccess) return -1;
+    spill_cap = (uint32_t)cap;
+    return alloc_chunk_state() == hipSuccess ? 1 : -1;
+  }
+
   hipError_t alloc_chunk_state()
   {
     if (d_status) (void)hipFree(d_status), d_status = nullptr;
@@ -270,8 +284,10 @@ struct Pipeline {
     hipError_t e = hipMalloc(&d_status, status_words * 8);
     if (e != hipSuccess) return e;
     const size_t ol_cells = std::max((size_t)geom.nbricks * cap_per_brick, (size_t)sgeom.ntiles * spl_cap);
-    archive_cap = 176 + (size_t)elem_bytes * sgeom.anchor_len + 128 + rvbk_bytes(kMaxBklen) + 8 * (size_t)pardeg +
-                  4 * bitstream_cells_cap() + 8 * (ol_cells + spill_cap) + 64;
+    // chunk tables: the tuned chunking's, or the brick layout's (one chunk per brick row)
+    const size_t chunks = std::max((size_t)pardeg, bl.g.ok ? (size_t)bl.g.nchunks : 0);
+    archive_cap = 176 + (size_t)elem_bytes * sgeom.anchor_len + 128 + rvbk_bytes(kMaxBklen) + 8 * chunks +
+                  4 * (bitstream_cells_cap() + chunks) + 8 * (ol_cells + spill_cap) + 64;
     return hipMalloc(&d_archive, archive_cap);
   }
 
@@ -329,10 +345,21 @@ struct Pipeline {
   template <typename T>
   int compress(psz_header* h, const T* in, uint8_t** out, size_t* outlen)
   {
-    if (codebook == PSZ_AMD_CODEBOOK_SAMPLED && bl.g.ndim == 3 && use_brick(h->pipeline.predictor))
-      return compress_sampled<T>(h, in, out, outlen);
-    const int s = compress_scan<T>(h, in, true);
-    return s ? s : compress_finish(h, nullptr, out, outlen);
+    const psz_rc2 rc = h->rc;  // Rel mode scales eb in place: a second run starts from the caller's
+    for (int run = 0;; run++) {
+      const uint32_t cap0 = spill_cap;
+      int s;
+      if (codebook == PSZ_AMD_CODEBOOK_SAMPLED && bl.g.ndim == 3 && use_brick(h->pipeline.predictor))
+        s = compress_sampled<T>(h, in, out, outlen);
+      else {
+        s = compress_scan<T>(h, in, true);
+        if (!s) s = compress_finish(h, nullptr, out, outlen);
+      }
+      // more outliers than the spill list held: it has grown to hold them all, compress again
+      // (identical below the reference's 10 % cap, where this never runs)
+      if (s != PSZ_WARN_OUTLIER_TOO_MANY || spill_cap == cap0 || run > 0) return s;
+      h->rc = rc;
+    }
   }
 
   // Pass 1: [extrema] -> predict + histogram + outliers (+ codes).  The histogram stays on the
@@ -722,7 +749,14 @@ struct Pipeline {
       std::fprintf(stderr, "[cusz_amd] encoder reservation/look-back check failed\n");
       return PSZ_AMD_ERR_ENCODER;
     }
-    if (ci.outlier_lost) return PSZ_WARN_OUTLIER_TOO_MANY;
+    if (ci.outlier_lost) {
+      // the spill list was too small for this field's outliers (every cell was counted): grow it
+      // (and the archive) to hold them all; compress() then runs once more, a scan/finish caller
+      // gets the warning and may repeat the call
+      const int g = grow_spill((uint64_t)spill_cap + ci.outlier_lost);
+      if (g < 0) return PSZ_AMD_ERR_DEVICE;
+      return PSZ_WARN_OUTLIER_TOO_MANY;
+    }
     *out = d_archive;
     *outlen = h->entry[PSZHEADER_ENC_PASS2_END];
     return PSZ_SUCCESS;

@@ -74,3 +74,40 @@ def test_nyx_six_fields_sharded_equals_whole():
     for r in res:
         r.close()
     whole.close()
+
+
+def test_nyx_velocity_abs_1e4_beyond_outlier_cap(oracle):
+    """SURVEY §8d's config-4 bound, abs 1e-4, on a Nyx-like velocity field (200 G): most elements
+    are outliers, far past the reference's 10 % capacity (buf_comp.cc:87-88).  The capacity grows:
+    on a tile-aligned slab the codes and outliers equal the oracle's and the field decompresses
+    within the bound; the full 512 x 512 x 64 slab of an 8-rank run decompresses within it too."""
+    small = (256, 64, 16)
+    v = datagen.nyx_fields_torch((256, 64, 16), device="cuda")[1].contiguous()
+    r = cz.Resource(cz.F4, small)
+    ptr, nb, st = r.compress(v.data_ptr(), 1e-4)
+    assert st == cz.PSZ_SUCCESS
+    host = v.cpu().numpy()
+    codes, ov, oi = oracle.lorenzo_c(host, small, 1e-4)
+    assert r.header.splen == len(oi) > host.size // 10
+    r.decode_codes(ptr)
+    sync()
+    got = d2h(r.internals().d_quant_codes, 2 * host.size, np.uint16)
+    np.testing.assert_array_equal(got, codes)
+    out = torch.empty(host.size, dtype=torch.float32, device="cuda")
+    ptr, nb, st = r.compress(v.data_ptr(), 1e-4)
+    r.decompress(ptr, nb, out.data_ptr())
+    sync()
+    np.testing.assert_array_equal(out.cpu().numpy(), oracle.lorenzo_x(codes, ov, oi, small, 1e-4))
+    r.close()
+
+    slab = (512, 512, 64)
+    f = datagen.nyx_fields_torch(FULL, device="cuda", z0=0, z1=64)[1].contiguous()
+    r = cz.Resource(cz.F4, slab)
+    ptr, nb, st = r.compress(f.data_ptr(), 1e-4)
+    assert st == cz.PSZ_SUCCESS and r.header.splen > f.numel() // 10
+    out = torch.empty(f.numel(), dtype=torch.float32, device="cuda")
+    r.decompress(ptr, nb, out.data_ptr())
+    sync()
+    err = (out.double() - f.double()).abs().max().item()
+    assert err <= 1e-4 * 1.001 + 2.0 ** -23 * f.abs().max().item(), err
+    r.close()

@@ -75,15 +75,24 @@ def test_spline_parity(oracle, dims, dtype, eb):
     assert err <= tol * ebx, (err / ebx, nol)
 
 
-def test_spline_too_many_outliers():
-    """More than 10 % outliers -> PSZ_WARN_OUTLIER_TOO_MANY (the reference's cap, buf_comp.hh:55)."""
+def test_spline_beyond_ten_percent_outliers():
+    """More than the reference's 10 % outliers (buf_comp.hh:55): the capacity grows, the archive
+    is valid and decompresses within the bound (float rounding: spline f32 tolerance)."""
+    import torch
+
     dims = (70, 19, 13)
     data = datagen.smooth3d_np(dims, 5)
     r = cz.Resource(cz.F4, dims, cz.Spline)
     d_in = to_device(data)
-    with pytest.raises(cz.PszError) as e:
-        r.compress(d_in.data_ptr(), 1e-6, cz.Abs)
-    assert e.value.status == cz.PSZ_WARN_OUTLIER_TOO_MANY
+    ptr, nb, st = r.compress(d_in.data_ptr(), 1e-6, cz.Abs)
+    assert st == cz.PSZ_SUCCESS
+    assert r.header.splen > data.size // 10
+    out = torch.empty(data.size, dtype=torch.float32, device="cuda")
+    r.decompress(ptr, nb, out.data_ptr())
+    sync()
+    err = np.abs(out.cpu().numpy().astype(np.float64) - data).max()
+    # eb = 1e-6 is ~8 f32 ulps of these values: the float reconstruction's rounding adds a few
+    assert err <= 1e-6 + 4 * 2.0 ** -23 * np.abs(data).max(), err
     r.close()
 
 
