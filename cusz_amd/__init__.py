@@ -227,7 +227,8 @@ class Resource:
         return out.value, nbytes.value, st
 
     def compress_scan(self, d_in: int, eb: float, d_hist: int, mode: int = Abs, radius: int = 512):
-        """Pass 1 of a sharded compress: the slab's histogram u32[2 radius] goes to d_hist."""
+        """Pass 1 of a sharded compress: the slab's histogram u32[2 radius] goes to d_hist, then
+        one more word (outlier cells beyond this slab's capacity); d_hist holds 2 radius + 1."""
         f = lib().psz_amd_compress_scan_float if self.dtype == F4 else lib().psz_amd_compress_scan_double
         st = f(self._h, psz_rc2(mode, eb, radius), C.c_void_p(d_in), C.c_void_p(d_hist))
         if st not in (PSZ_SUCCESS, PSZ_WARN_RADIUS_TOO_LARGE):
@@ -235,7 +236,9 @@ class Resource:
         return st
 
     def compress_finish(self, d_hist: int = 0):
-        """Codebook from the device histogram d_hist (0: the slab's own) -> archive."""
+        """Codebook from the device histogram d_hist (u32[2 radius + 1]: the summed slab histograms
+        and overflow words; 0: the slab's own) -> archive.  PszError(PSZ_WARN_OUTLIER_TOO_MANY)
+        when a slab overflowed its outlier capacity: repeat scan and finish (it has grown)."""
         out = C.c_void_p()
         nbytes = C.c_size_t()
         st = lib().psz_amd_compress_finish(self._h, C.c_void_p(d_hist or None), C.byref(self.header),

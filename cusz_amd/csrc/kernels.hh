@@ -138,6 +138,7 @@ int launch_upload(const XferRegions& r, hipStream_t st);
 int launch_gate_upload(const XferRegions& r, const uint32_t* gate, uint32_t epoch, unsigned int* timeout,
                        hipStream_t st);
 int launch_zero(const XferRegions& r, hipStream_t st);  // dst/nwords only
+int launch_excess(const uint32_t* spill_cnt, uint32_t cap, uint32_t* dst, hipStream_t st);
 
 // ---- cuSZ-i spline3 (spline.hip) -----------------------------------------------------------
 struct SplineGeom {

@@ -134,7 +134,7 @@ struct Pipeline {
   uint32_t* h_hist() { return reinterpret_cast<uint32_t*>(h_xfer + 64); }               // 4 KB
   uint32_t* h_book() { return reinterpret_cast<uint32_t*>(h_xfer + 64 + 4096); }        // 4 KB
   uint8_t* h_revbook() { return h_xfer + 64 + 8192; }                                    // 2304 B
-  uint8_t* h_readback() { return h_xfer + 64 + 8192 + 2560; }                            // 1 KB
+  uint8_t* h_readback() const { return h_xfer + 64 + 8192 + 2560; }                            // 1 KB
 
   bool timing = false;
   hipEvent_t ev[12] = {};
@@ -241,7 +241,7 @@ struct Pipeline {
     // codes: index order (reference layout) or brick order (brick layout: whole bricks)
     const size_t code_len = std::max(n + 64, bl.g.ok ? (size_t)bl.g.nbricks * bl.g.brick_elems : 0);
     CUSZ_AMD_HIP_CHECK(hipMalloc(&d_codes, code_len * sizeof(uint16_t)));
-    CUSZ_AMD_HIP_CHECK(hipMalloc(&d_hist, kMaxBklen * sizeof(uint32_t)));
+    CUSZ_AMD_HIP_CHECK(hipMalloc(&d_hist, (kMaxBklen + 4) * sizeof(uint32_t)));  // + the sharded overflow word
     CUSZ_AMD_HIP_CHECK(hipMalloc(&d_book, kMaxBklen * sizeof(uint32_t)));
     CUSZ_AMD_HIP_CHECK(hipMalloc(&d_slots, slot_cells * 8));
     CUSZ_AMD_HIP_CHECK(hipMalloc(&d_brick_cnt, (size_t)max_bricks * 4));
@@ -339,6 +339,7 @@ struct Pipeline {
     bool active = false, brick = false, spl = false, zz = false;
     int radius = 0;
     uint32_t hist_epoch = 0;  // != 0: the scan published d_hist to h_hist() with this epoch (flag 2)
+    bool ext = false;         // finish with a caller's (reduced) histogram + overflow word
     size_t anchor_bytes = 0;
   } pend;
 
@@ -370,6 +371,7 @@ struct Pipeline {
   int compress_scan(psz_header* h, const T* in, bool pub_hist = false)
   {
     pend.active = false;
+    pend.ext = false;
     const psz_predictor pred = h->pipeline.predictor;
     if (pred != Lorenzo && pred != LorenzoZigZag && pred != Spline) return PSZ_ABORT_NO_SUCH_PREDICTOR;
     if (h->pipeline.codec1 != Huffman) return PSZ_ABORT_NO_SUCH_CODEC;
@@ -413,9 +415,9 @@ struct Pipeline {
     // per-call state reset (the reference never resets these: SURVEY.md Appendix B.3)
     if (brick)
       CUSZ_AMD_HIP_CHECK((hipError_t)launch_zero(
-          regions({{d_hist, nullptr, (size_t)bklen * 4}, {d_small, nullptr, 64 + sizeof(CompressInfo)}}), stream));
+          regions({{d_hist, nullptr, (size_t)(bklen + 1) * 4}, {d_small, nullptr, 64 + sizeof(CompressInfo)}}), stream));
     else
-      CUSZ_AMD_HIP_CHECK((hipError_t)launch_zero(regions({{d_hist, nullptr, (size_t)bklen * 4},
+      CUSZ_AMD_HIP_CHECK((hipError_t)launch_zero(regions({{d_hist, nullptr, (size_t)(bklen + 1) * 4},
                                                           {d_small, nullptr, 64 + sizeof(CompressInfo)},
                                                           {d_status, nullptr, status_words * 8}}),
                                                  stream));
@@ -479,8 +481,10 @@ struct Pipeline {
     if (!pend.active) return PSZ_AMD_ERR_STATE;
     pend.active = false;
     const int radius = pend.radius, bklen = 2 * radius;
+    pend.ext = ext_hist != nullptr;
     if (ext_hist) {
-      CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(d_hist, ext_hist, (size_t)bklen * 4, hipMemcpyDeviceToDevice, stream));
+      // bklen counts + the summed overflow word of every slab (psz_amd_compress_scan_*)
+      CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(d_hist, ext_hist, (size_t)(bklen + 1) * 4, hipMemcpyDeviceToDevice, stream));
       pend.hist_epoch = 0;  // the scan's published histogram is not the one to encode with
     }
     if (pend.brick) return compress_brick(h, out, outlen, radius);
@@ -494,7 +498,7 @@ struct Pipeline {
     uint32_t* spill_start = spl ? d_spl_sps : nullptr;
 
     // codebook on the host (hf_hl.cc:21-34), one round trip
-    int fs = fetch(regions({{h_hist(), d_hist, (size_t)bklen * 4}}), 2);
+    int fs = fetch(hist_regions(bklen), 2);
     if (fs) return fs;
     const int rv = build_codebook(h_hist(), bklen, h_book(), h_revbook());
     const size_t phf_off = 176 + anchor_bytes;  // anchors: spline only (compressor.inl:160)
@@ -563,8 +567,7 @@ struct Pipeline {
     uint32_t eh = pend.hist_epoch;  // published by the scan's last workgroup, or now
     if (!eh) {
       eh = ++epoch;
-      CUSZ_AMD_HIP_CHECK((hipError_t)launch_publish(regions({{h_hist(), d_hist, (size_t)bklen * 4}}),
-                                                    const_cast<uint32_t*>(flag(2)), eh, stream));
+      CUSZ_AMD_HIP_CHECK((hipError_t)launch_publish(hist_regions(bklen), const_cast<uint32_t*>(flag(2)), eh, stream));
     }
     const uint32_t eg = ++gate_epoch;
     const bool gated = gate;
@@ -714,6 +717,14 @@ struct Pipeline {
   }
 
   // read back the device-written header + summary (one flag wait), report status
+  // the histogram for the host codebook, and with a caller's reduced histogram its overflow word
+  XferRegions hist_regions(int bklen)
+  {
+    if (pend.ext) return regions({{h_hist(), d_hist, (size_t)bklen * 4}, {h_readback() + 448, d_hist + bklen, 4}});
+    return regions({{h_hist(), d_hist, (size_t)bklen * 4}});
+  }
+  uint32_t global_excess() const { return pend.ext ? *reinterpret_cast<const uint32_t*>(h_readback() + 448) : 0u; }
+
   XferRegions readback_regions()
   {
     return regions({{h_readback(), d_archive, 176},
@@ -752,11 +763,14 @@ struct Pipeline {
     if (ci.outlier_lost) {
       // the spill list was too small for this field's outliers (every cell was counted): grow it
       // (and the archive) to hold them all; compress() then runs once more, a scan/finish caller
-      // gets the warning and may repeat the call
+      // gets the warning and repeats scan and finish
       const int g = grow_spill((uint64_t)spill_cap + ci.outlier_lost);
       if (g < 0) return PSZ_AMD_ERR_DEVICE;
       return PSZ_WARN_OUTLIER_TOO_MANY;
     }
+    // a sharded finish: another slab overflowed (the summed overflow word), so every rank sees
+    // the warning and repeats the step together
+    if (global_excess()) return PSZ_WARN_OUTLIER_TOO_MANY;
     *out = d_archive;
     *outlen = h->entry[PSZHEADER_ENC_PASS2_END];
     return PSZ_SUCCESS;
@@ -1049,8 +1063,10 @@ static int export_hist(psz_resource* m, uint32_t* d_out, int status)
 {
   Pipeline* p = cusz_amd::P(m);
   if (!d_out) return PSZ_AMD_ERR_INVALID_ARG;
-  CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(d_out, p->d_hist, sizeof(uint32_t) * 2 * m->header->rc.radius,
-                                    hipMemcpyDeviceToDevice, p->stream));
+  const int bklen = 2 * m->header->rc.radius;
+  CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(d_out, p->d_hist, sizeof(uint32_t) * bklen, hipMemcpyDeviceToDevice, p->stream));
+  // word bklen: this slab's outlier cells beyond its spill list (summed with the histograms)
+  CUSZ_AMD_HIP_CHECK((hipError_t)cusz_amd::launch_excess(p->spill_cnt(), p->spill_cap, d_out + bklen, p->stream));
   return status;
 }
 

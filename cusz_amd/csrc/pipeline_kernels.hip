@@ -310,6 +310,21 @@ int launch_zero(const XferRegions& r, hipStream_t st)
   return (int)hipGetLastError();
 }
 
+// the sharded compress's overflow word: outlier cells of the last pass 1 beyond the spill list
+__global__ void k_excess(const uint32_t* spill_cnt, uint32_t cap, uint32_t* dst)
+{
+  if (threadIdx.x == 0) {
+    const uint32_t c = *spill_cnt;
+    *dst = c > cap ? c - cap : 0u;
+  }
+}
+
+int launch_excess(const uint32_t* spill_cnt, uint32_t cap, uint32_t* dst, hipStream_t st)
+{
+  k_excess<<<1, 64, 0, st>>>(spill_cnt, cap, dst);
+  return (int)hipGetLastError();
+}
+
 int launch_upload(const XferRegions& r, hipStream_t st)
 {
   k_upload<<<4, 256, 0, st>>>(r);

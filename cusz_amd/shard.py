@@ -142,23 +142,40 @@ def compress_fields_sharded(resources, fields, eb, dist, mode=0, radius=512, dev
     ValueError otherwise): RCCL orders the all-reduce after the scans and the finish after the
     all-reduce on that stream, so no host synchronisation is needed between the phases.  The u32 histogram sums are
     reduced as int32 (the bit pattern is the u32 sum: every count is < 2^32).
+    A slab with more outliers than its capacity (past the reference's 10 %) makes every rank's
+    finish warn through the summed overflow word (column 2 radius of `hists`); every rank then
+    repeats its scans, the all-reduce and its finishes once, with the grown capacity.
     Returns [(archive_ptr, nbytes)] (device archives, valid until the manager's next compress)."""
     import torch
+
+    from . import PSZ_WARN_OUTLIER_TOO_MANY, PszError
 
     bklen = 2 * radius
     f = len(resources)
     check_streams(resources, device if device is not None else (fields[0].device if fields else None))
     ebs = [eb * r for r in global_value_ranges(resources, fields, dist)] if mode == 1 else [eb] * f
     if hists is None:
-        hists = torch.empty((f, bklen), dtype=torch.int32, device=device)
-    for i, (r, t) in enumerate(zip(resources, fields)):
-        r.compress_scan(t.data_ptr(), ebs[i], hists[i].data_ptr(), 0, radius)
-    if dist is not None and dist.get_world_size() > 1:
-        allreduce_histograms(hists, dist)
-    out = []
-    for i, r in enumerate(resources):
-        ptr, nb, _ = r.compress_finish(hists[i].data_ptr())
-        out.append((ptr, nb))
+        hists = torch.empty((f, bklen + 1), dtype=torch.int32, device=device)
+    assert hists.shape[-1] == bklen + 1, "histogram rows hold 2 radius counts + the overflow word"
+    for attempt in range(2):
+        for i, (r, t) in enumerate(zip(resources, fields)):
+            r.compress_scan(t.data_ptr(), ebs[i], hists[i].data_ptr(), 0, radius)
+        if dist is not None and dist.get_world_size() > 1:
+            allreduce_histograms(hists, dist)  # the overflow words are summed with the counts
+        out, again = [], False
+        for i, r in enumerate(resources):
+            try:
+                ptr, nb, _ = r.compress_finish(hists[i].data_ptr())
+            except PszError as e:
+                # a slab had more outliers than its capacity (past the reference's 10 %): every
+                # rank sees it through the summed overflow word; the capacity has grown
+                if e.status != PSZ_WARN_OUTLIER_TOO_MANY or attempt:
+                    raise
+                again = True
+                continue
+            out.append((ptr, nb))
+        if not again:
+            return out
     return out
 
 

@@ -107,10 +107,14 @@ int psz_amd_set_codebook(psz_resource* m, int mode);
  * A field split into tile-aligned slabs (z: multiples of 8 planes) is compressed one slab per
  * GPU with ONE codebook:
  *   1. psz_amd_compress_scan_*: pass 1 only (predict, histogram, outliers); the slab's
- *      histogram u32[2 * radius] is copied to OUT_d_hist (device, on the manager's stream).
- *   2. the caller sums the histograms of all slabs (e.g. an RCCL all-reduce).
- *   3. psz_amd_compress_finish: codebook from IN_d_hist (device u32[2 * radius]; NULL: the
- *      slab's own histogram), encode, archive -- outputs as psz_compress_float.
+ *      histogram u32[2 * radius] is copied to OUT_d_hist (device, on the manager's stream),
+ *      followed by one more word: the slab's outlier cells beyond its current capacity.
+ *   2. the caller sums these u32[2 * radius + 1] of all slabs (e.g. an RCCL all-reduce).
+ *   3. psz_amd_compress_finish: codebook from IN_d_hist (device u32[2 * radius + 1]; NULL: the
+ *      slab's own histogram), encode, archive -- outputs as psz_compress_float.  When the last
+ *      word is nonzero (some slab had more outliers than its capacity: past the reference's
+ *      10 %), every slab's finish returns PSZ_WARN_OUTLIER_TOO_MANY, the slabs that overflowed
+ *      have grown their capacity, and repeating steps 1-3 succeeds on every rank together.
  * psz_compress_analyize_float (cusz_rev1.h) is step 1 with the histogram exported to the host
  * (compressor.inl:305-337). */
 int psz_amd_compress_scan_float(psz_resource* m, psz_rc2 rc, float* IN_d_data, uint32_t* OUT_d_hist);

@@ -16,7 +16,7 @@ dims = (512, 512, 512)
 x = datagen.smooth3d_torch(dims, seed=2)
 st = torch.cuda.current_stream()
 r = cz.Resource(cz.F4, dims, stream=st.cuda_stream)
-hist = torch.zeros(1024, dtype=torch.int32, device="cuda")
+hist = torch.zeros(1025, dtype=torch.int32, device="cuda")  # counts + overflow word
 ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
 
 

@@ -27,7 +27,7 @@ def test_nyx_six_fields_sharded_equals_whole():
     res = [cz.Resource(cz.F4, s.dims, stream=st) for s in slabs]
     whole = cz.Resource(cz.F4, FULL, stream=st)
     out = torch.empty(FULL[0] * FULL[1] * FULL[2], dtype=torch.float32, device="cuda")
-    hists = torch.zeros((WORLD, 1024), dtype=torch.int32, device="cuda")
+    hists = torch.zeros((WORLD, 1025), dtype=torch.int32, device="cuda")
     mm = torch.empty((WORLD, 2), dtype=torch.float64, device="cuda")
     r2r = 1e-4
     fields = datagen.nyx_fields_torch(FULL, device="cuda")
@@ -44,7 +44,7 @@ def test_nyx_six_fields_sharded_equals_whole():
             r.compress_scan(v.data_ptr(), eb, hists[k].data_ptr())
         sync()
         g = hists.to(torch.int64).sum(0)
-        assert int(g.sum().item()) == f.numel()
+        assert int(g[:1024].sum().item()) == f.numel() and int(g[1024].item()) == 0
         g32 = g.to(torch.int32).contiguous()
         parts = []
         for r in res:

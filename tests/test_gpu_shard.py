@@ -28,7 +28,7 @@ def _whole(data, dims, eb, dtype, layout, sublen):
 def _sharded(data, dims, world, eb, dtype, layout, sublen):
     slabs = [s for s in plan_slabs(dims, world) if s.count]
     res, dins = [], []
-    hists = torch.zeros((len(slabs), 1024), dtype=torch.int32, device="cuda")
+    hists = torch.zeros((len(slabs), 1025), dtype=torch.int32, device="cuda")  # + the overflow word
     for i, s in enumerate(slabs):
         r = cz.Resource(cz.F4 if dtype == np.float32 else cz.F8, s.dims)
         r.set_layout(layout)
@@ -77,12 +77,12 @@ def test_scan_then_finish_equals_compress():
     single, _ = _whole(data, dims, 1e-4, np.float32, cz.LAYOUT_BRICK, 0)
     r = cz.Resource(cz.F4, dims)
     d = to_device(data)
-    h = torch.zeros(1024, dtype=torch.int32, device="cuda")
+    h = torch.zeros(1025, dtype=torch.int32, device="cuda")
     r.compress_scan(d.data_ptr(), 1e-4, h.data_ptr())
     ptr, nb, _ = r.compress_finish(0)  # the slab's own histogram
     assert d2h(ptr, nb).tobytes() == single
     sync()
-    assert int(h.sum().item()) == data.size  # the exported slab histogram
+    assert int(h[:1024].sum().item()) == data.size and int(h[1024].item()) == 0  # counts, no overflow
 
 
 def test_analyze_exports_histogram(oracle):
@@ -96,3 +96,42 @@ def test_analyze_exports_histogram(oracle):
     assert st == cz.PSZ_SUCCESS
     codes, _, _ = oracle.lorenzo_c(data, dims, 1e-4)
     np.testing.assert_array_equal(hist, oracle.histogram(codes))
+
+
+def test_sharded_outlier_overflow_repeats_together():
+    """One slab past its outlier capacity (uniform noise), the other well within it: the summed
+    overflow word makes BOTH finishes warn, the overflowing slab's capacity grows, and the
+    repeated step gives archives that merge into the whole field's archive (error-bounded)."""
+    dims = (4096, 1, 1)
+    rng = np.random.default_rng(11)
+    data = np.concatenate([np.cumsum(rng.normal(0, 1e-5, 2048)), rng.uniform(-1e3, 1e3, 2048)]).astype(np.float32)
+    slabs = plan_slabs(dims, 2)
+    res = [cz.Resource(cz.F4, s.dims) for s in slabs]
+    dins = [to_device(data[s.offset:s.offset + s.count]) for s in slabs]
+    hists = torch.zeros((2, 1025), dtype=torch.int32, device="cuda")
+    for attempt in range(2):
+        for i, r in enumerate(res):
+            r.compress_scan(dins[i].data_ptr(), 1e-4, hists[i].data_ptr())
+        sync()
+        g = hists.to(torch.int64).sum(0).to(torch.int32).contiguous()
+        if attempt == 0:
+            assert int(g[1024].item()) > 0  # slab 1 overflowed
+        sts, parts = [], []
+        for r in res:
+            try:
+                ptr, nb, _ = r.compress_finish(g.data_ptr())
+                parts.append(d2h(ptr, nb).tobytes())
+                sts.append(cz.PSZ_SUCCESS)
+            except cz.PszError as e:
+                sts.append(e.status)
+        if attempt == 0:
+            assert sts == [cz.PSZ_WARN_OUTLIER_TOO_MANY] * 2
+    assert sts == [cz.PSZ_SUCCESS] * 2
+    merged = cz.merge_archives(parts, dims, [s.offset for s in slabs])
+    hdr = cz.psz_header.from_buffer_copy(merged[:176])
+    rf = cz.Resource(cz.F4, dims, header=hdr)
+    d_arch = torch.frombuffer(bytearray(merged), dtype=torch.uint8).to("cuda")
+    out = torch.empty(dims[0], dtype=torch.float32, device="cuda")
+    rf.decompress(d_arch.data_ptr(), len(merged), out.data_ptr())
+    sync()
+    assert np.abs(out.cpu().numpy().astype(np.float64) - data).max() <= 1.001e-4
