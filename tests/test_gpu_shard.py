@@ -102,9 +102,10 @@ def test_sharded_outlier_overflow_repeats_together():
     """One slab past its outlier capacity (uniform noise), the other well within it: the summed
     overflow word makes BOTH finishes warn, the overflowing slab's capacity grows, and the
     repeated step gives archives that merge into the whole field's archive (error-bounded)."""
-    dims = (4096, 1, 1)
+    dims = (131072, 1, 1)
     rng = np.random.default_rng(11)
-    data = np.concatenate([np.cumsum(rng.normal(0, 1e-5, 2048)), rng.uniform(-1e3, 1e3, 2048)]).astype(np.float32)
+    h = dims[0] // 2
+    data = np.concatenate([np.cumsum(rng.normal(0, 1e-5, h)), rng.uniform(-1e3, 1e3, h)]).astype(np.float32)
     slabs = plan_slabs(dims, 2)
     res = [cz.Resource(cz.F4, s.dims) for s in slabs]
     dins = [to_device(data[s.offset:s.offset + s.count]) for s in slabs]
@@ -134,4 +135,5 @@ def test_sharded_outlier_overflow_repeats_together():
     out = torch.empty(dims[0], dtype=torch.float32, device="cuda")
     rf.decompress(d_arch.data_ptr(), len(merged), out.data_ptr())
     sync()
-    assert np.abs(out.cpu().numpy().astype(np.float64) - data).max() <= 1.001e-4
+    # f32 reconstruction at |x| ~ 1e3: its rounding adds to the bound (as bench.py's check)
+    assert np.abs(out.cpu().numpy().astype(np.float64) - data).max() <= 1.001e-4 + 2.0 ** -23 * np.abs(data).max()
