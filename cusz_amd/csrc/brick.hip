@@ -265,8 +265,8 @@ __device__ __forceinline__ void finish_unit(const OutlierSink& ol, const BrickCo
 // the previous row of the same y-step and the y-diff against row (y - 1, z) kept in registers
 // (bprev).  kScanAhead rows (two y-steps) are in flight per wave, loaded into a register queue
 // whose slot is the row's position modulo kScanAhead (the row loop is unrolled by kScanAhead, so
-// the queue needs no copies); the loads run across brick boundaries.  About 110 VGPRs: four
-// waves per SIMD.
+// the queue needs no copies); the loads run across brick boundaries.  f32: capped at 128 VGPRs
+// (4 waves per SIMD: a 512^3 field's 8192 bricks are exactly two rounds of the 4096 waves).
 template <typename T>
 #ifndef CUSZ_AMD_SCAN_AHEAD
 #define CUSZ_AMD_SCAN_AHEAD 8
@@ -275,6 +275,7 @@ constexpr int kScanAhead = sizeof(T) == 4 ? CUSZ_AMD_SCAN_AHEAD : 8;
 
 template <typename T, int V, bool ZZ>
 __global__ void __launch_bounds__(64 * kBrickWaves)
+__attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? 4 : 1)))  // f32: <= 128 VGPRs, 4 waves per SIMD
 k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T ebx2_r, T r, OutlierSink ol,
               uint32_t* __restrict__ g_hist, uint16_t* __restrict__ bhist, BrickCodes bcs, int bklen,
               uint32_t nbx, uint32_t nby, uint32_t nbricks, HostPub pub)
@@ -700,11 +701,19 @@ constexpr int pack_cells_words()
 {  // worst case cells of one row (27-bit codes) + slack, multiple of 4
   return ((64 * V * kLmax + 31) / 32 + 4 + 3) / 4 * 4;
 }
+constexpr int kPackRowMax = (64 * 4 * kLmax + 31) / 32 + 1;  // words one row's packing may touch
+constexpr int kPackCells = 768;  // per-wave LDS cell buffer (words): rows accumulate until a flush
+constexpr int kPackLdsWords = kMaxBklen + 256 + kBrickWaves * kPackCells;  // 19 KiB: 8 workgroups per CU
+static_assert(kPackCells >= 2 * kPackRowMax, "a flush every row or two at worst");
 
 // Pass 2 packs the brick's rows from the codes pass 1 left in brick order (row r of brick b at
-// (b * 64 + r) * W): per row, codewords -> wave scan of their lengths -> MSB-first packing into
-// LDS cells (each row starts a new cell, hf_kernels.cuhip.inl:97-157) -> one coalesced copy.
-// The codes of the next y-step are loaded while the current one is packed.
+// (b * 64 + r) * W): per row, codewords (byte rows through a 256-entry table of the byte window)
+// -> wave scan of their lengths -> MSB-first packing into the wave's LDS cell buffer (each row
+// starts a new cell, hf_kernels.cuhip.inl:97-157).  Rows accumulate back to back in the buffer;
+// it is copied to the brick's region in coalesced 256-B stores when the next row might not fit
+// and at the brick's end.  Each row's load is issued when the same z of the previous y-step is
+// consumed (8 rows in flight).  About 60 VGPRs: 8 waves per SIMD, one brick per wave on a 512^3
+// field (no second round of waves).
 template <int V, int ND>
 __global__ void __launch_bounds__(64 * kBrickWaves)
 k_brick3_pack(BrickCodes bcs, uint32_t ly, uint32_t lz, const uint32_t* __restrict__ book,
@@ -713,15 +722,19 @@ k_brick3_pack(BrickCodes bcs, uint32_t ly, uint32_t lz, const uint32_t* __restri
               unsigned int* overflow, HostPub pub)
 {
   static_assert(V == 4, "8-B code loads");
-  constexpr int CW = pack_cells_words<V>();
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t* s_book = smem;  // kMaxBklen words
+  uint32_t* s_book = smem;             // kMaxBklen words: book word by code
+  uint32_t* s_b8 = smem + kMaxBklen;   // 256 words: book word by byte code (255: code 0)
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wid: uniform (SGPR)
-  uint32_t* cells = smem + kMaxBklen + wid * CW;
-  for (int i = threadIdx.x; i < bklen; i += blockDim.x) s_book[i] = book[i];
-  for (int i = lane; i < CW; i += 64) cells[i] = 0;
+  uint32_t* cells = smem + kMaxBklen + 256 + wid * kPackCells;
+  const uint32_t nw = gridDim.x * kBrickWaves;  // (read before the divergent fill loops)
+  for (int i = threadIdx.x; i < bklen; i += 64 * kBrickWaves) s_book[i] = book[i];
+  for (int i = threadIdx.x; i < 256; i += 64 * kBrickWaves) {
+    const uint32_t c = i == 255 ? 0u : (uint32_t)i + bcs.c0;
+    s_b8[i] = c < (uint32_t)bklen ? book[c] : 0u;
+  }
+  for (int i = lane; i < kPackCells; i += 64) cells[i] = 0;
   __syncthreads();
-  const uint32_t nw = gridDim.x * kBrickWaves;
   const uint32_t ncell = pl.cell_pre[pl.nblk];
   uint2* ol_dst = reinterpret_cast<uint2*>(bitstream + ncell);  // outlier cells follow the bitstream
   {  // spill list (bricks past their slot; not expected below 10 % outliers) after every slot
@@ -746,7 +759,24 @@ k_brick3_pack(BrickCodes bcs, uint32_t ly, uint32_t lz, const uint32_t* __restri
       }
     }
     uint32_t* dst = bitstream + base;
-    uint32_t off = 0;
+    uint32_t off = 0;    // region words packed (buffered or copied)
+    uint32_t fbase = 0;  // region word at the buffer's start
+    // buffered words [fbase, off) -> the region (never past lim: the region is an upper bound, so
+    // the clamp only guards a corrupt plan), buffer cleared
+    auto flush = [&]() {
+      hfd::wave_sync();
+      const uint32_t n = off - fbase, nst = fbase >= lim ? 0u : min(n, lim - fbase);
+      for (uint32_t i0 = 0; i0 < n; i0 += 64) {  // uniform trip count
+        const uint32_t i = i0 + (uint32_t)lane;
+        if (i < n) {
+          const uint32_t v = cells[i];
+          cells[i] = 0;
+          if (i < nst) dst[fbase + i] = v;
+        }
+      }
+      fbase = off;
+      hfd::wave_sync();
+    };
     const uint32_t bend = min((unit + 1) * kUnitBricks, nbricks);
     for (uint32_t brick = unit * kUnitBricks; brick < bend; brick++) {
       const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
@@ -767,57 +797,56 @@ k_brick3_pack(BrickCodes bcs, uint32_t ly, uint32_t lz, const uint32_t* __restri
         __builtin_memcpy(&v, a, 8);
         return v;
       };
-      uint32_t my_nbit = 0, my_entry = 0;
-      uint2 cur[8], nxt[8];
+      uint32_t my_nbit = 0, my_entry = 0;  // lane r: row r's bits and first cell
+      // Straight-line row loop (no branch around a load: the compiler then waits for each row's
+      // own load, not for all of them): every row's load is issued, rows outside the field read
+      // a row of the brick's own code block and pack nothing.
+      uint2 qv[8];
 #pragma unroll
-      for (int z = 0; z < 8; z++) nxt[z] = row_ok(0, z) ? load_row(z) : make_uint2(0, 0);
+      for (int z = 0; z < 8; z++) qv[z] = load_row(z);
       for (uint32_t y = 0; y < nyv; y++) {
 #pragma unroll
-        for (int z = 0; z < 8; z++) cur[z] = nxt[z];
-        if (y + 1 < nyv)
-#pragma unroll
-          for (int z = 0; z < 8; z++) nxt[z] = row_ok(y + 1, z) ? load_row((y + 1) * 8 + z) : make_uint2(0, 0);
-#pragma unroll
         for (int z = 0; z < 8; z++) {
-          if (!row_ok(y, z)) break;
-          uint32_t qs[4];
-          if ((rm >> (y * 8 + z)) & 1ull) {
-            qs[0] = cur[z].x & 0xFFFFu, qs[1] = cur[z].x >> 16, qs[2] = cur[z].y & 0xFFFFu, qs[3] = cur[z].y >> 16;
+          const uint32_t row = y * 8 + z;
+          if (off - fbase + kPackRowMax > kPackCells) flush();
+          uint32_t w[V];
+          if ((rm >> row) & 1ull) {
+            w[0] = s_book[qv[z].x & 0xFFFFu], w[1] = s_book[qv[z].x >> 16];
+            w[2] = s_book[qv[z].y & 0xFFFFu], w[3] = s_book[qv[z].y >> 16];
           }
           else {
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-              const uint32_t b = (cur[z].x >> (8 * k)) & 255u;
-              qs[k] = b == 255u ? 0u : b + bcs.c0;  // 255: the outlier code 0
-            }
+            for (int k = 0; k < 4; k++) w[k] = s_b8[(qv[z].x >> (8 * k)) & 255u];
           }
-          uint32_t w[V], bits = 0;
-          // 1-D: the field's last chunk may be short; codes past its end get no codeword
-          const size_t cfirst = ((size_t)brick * 64u + y * 8u + (uint32_t)z) * (64u * V);
-          const bool short_row = ND == 1 && pl.n - cfirst < 64u * V;
+          qv[z] = load_row((row + 8) & 63u);
+          if (!row_ok(y, z)) {
 #pragma unroll
-          for (int k = 0; k < V; k++) {
-            w[k] = s_book[qs[k]];
-            if (short_row && cfirst + (uint32_t)lane * V + k >= pl.n) w[k] = 0;
-            bits += w[k] >> 27;
+            for (int k = 0; k < V; k++) w[k] = 0;
           }
+          // 1-D: the field's last chunk may be short; codes past its end get no codeword
+          if (ND == 1) {
+            const size_t cfirst = ((size_t)brick * 64u + row) * (64u * V);
+            if (pl.n - cfirst < 64u * V)
+#pragma unroll
+              for (int k = 0; k < V; k++)
+                if (cfirst + (uint32_t)lane * V + k >= pl.n) w[k] = 0;
+          }
+          uint32_t bits = 0;
+#pragma unroll
+          for (int k = 0; k < V; k++) bits += w[k] >> 27;
           const uint32_t inc = hfd::wave_incl_scan(bits);
           const uint32_t tot = readlane(inc, 63);
+          const uint32_t pos = ((off - fbase) << 5) + inc - bits;
           if (__builtin_expect(__builtin_amdgcn_ballot_w64(bits > 64u) == 0, 1))
-            hfd::pack4_or(cells, inc - bits, w, bits);
+            hfd::pack4_or(cells, pos, w, bits);
           else
-            hfd::pack_words<V>(cells, inc - bits, w, V);
-          hfd::wave_sync();
-          const uint32_t nc = (tot + 31) >> 5;
-          for (uint32_t i = lane; i < nc; i += 64) {
-            if (off + i < lim) dst[off + i] = cells[i];
-            cells[i] = 0;
-          }
-          if ((uint32_t)lane == y * 8 + z) my_nbit = tot, my_entry = base + off;
-          off += nc;
-          hfd::wave_sync();
+            hfd::pack_words<V>(cells, pos, w, V);
+          const uint32_t ent = base + off;
+          if ((uint32_t)lane == row) my_nbit = tot, my_entry = ent;
+          off += (tot + 31) >> 5;
         }
       }
+      flush();
       const uint32_t ry = lane >> 3, rz = lane & 7;
       if (row_ok(ry, rz) && ry < nyv) {
         const size_t c = ND == 1 ? (size_t)brick * 64u + (uint32_t)lane : ((size_t)(z0 + rz) * ly + (y0 + ry)) * nbx + bx;
@@ -2467,7 +2496,7 @@ int brick_configure(BrickLaunch& L, int elem_bytes, int device)
   L.ncu = ncu;
   int per_scan = 0, per_pack = 0;
   const size_t lds_scan = (size_t)(1 + kBrickWaves * kHistCopies) * kMaxBklen * 4;
-  const size_t lds_pack = ((size_t)kMaxBklen + (size_t)kBrickWaves * pack_cells_words<4>()) * 4;
+  const size_t lds_pack = (size_t)kPackLdsWords * 4;
   hipError_t e1, e2;
   if (elem_bytes == 8) {
     e1 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_scan, k_brick3_scan<double, 4, false>, 64 * kBrickWaves, lds_scan);
@@ -2538,7 +2567,7 @@ int launch_brick_pack(const BrickLaunch& L, const BrickCodes& bcodes, const uint
                       int reverse, unsigned int* overflow, hipStream_t st, const HostPub& pub)
 {
   const BrickGeom& g = L.g;
-  const size_t lds = ((size_t)kMaxBklen + (size_t)kBrickWaves * pack_cells_words<4>()) * 4;
+  const size_t lds = (size_t)kPackLdsWords * 4;
   if (g.ndim != 3)
     k_brick3_pack<4, 1><<<L.grid_pack, 64 * kBrickWaves, lds, st>>>(bcodes, L.ly, L.lz, book, bklen, plan, par_nbit,
                                                                     par_entry, bitstream, g.nbx, g.nby, g.nbricks,

@@ -26,71 +26,75 @@ constexpr int kLmax = 27;
 
 // 1-based binary min-heap of tree nodes with the reference's tie-breaking (qinsert / qremove,
 // hf_bk_impl1.seq.cc:103-137): a node moves up while its parent is strictly greater, down while
-// the smaller child (the right one only if strictly smaller) is strictly smaller.  Entries carry
-// their frequency, so no comparison goes through the node pool (same order of operations, so
-// the same heap states as the reference's pointer heap).
-struct HeapEntry {
-  uint64_t freq;
-  int32_t id;
-};
+// the smaller child (the right one only if strictly smaller) is strictly smaller.  An entry is
+// one u64, frequency << 12 | node id (frequencies are sums of u32 counts over <= 1024 symbols,
+// < 2^42; ids < 2 * 1024): comparisons look at the frequency only, so the heap goes through the
+// same states as the reference's pointer heap.
+constexpr int kIdBits = 12;
+constexpr int kMaxSym = 1 << 10;  // bklen <= 1024 (kMaxBklen)
 
-class MergeHeap {
- public:
-  explicit MergeHeap(HeapEntry* q) : q_(q) {}
+struct MergeHeap {
+  uint64_t q[2 * kMaxSym + 2];
+  int end = 1;
 
-  void push(uint64_t f, int32_t id)
+  static uint64_t freq(uint64_t e) { return e >> kIdBits; }
+
+  void push(uint64_t e)
   {
-    int i = end_++;
+    const uint64_t f = freq(e);
+    int i = end++;
     for (int j = i >> 1; j; j = i >> 1) {
-      if (q_[j].freq <= f) break;
-      q_[i] = q_[j];
+      if (freq(q[j]) <= f) break;
+      q[i] = q[j];
       i = j;
     }
-    q_[i] = {f, id};
+    q[i] = e;
   }
 
-  HeapEntry pop()
+  uint64_t pop()
   {
-    const HeapEntry top = q_[1];
-    const HeapEntry x = q_[--end_];
+    const uint64_t top = q[1];
+    const uint64_t x = q[--end], fx = freq(x);
     int i = 1;
-    for (int l = 2; l < end_; l = 2 * i) {
-      if (l + 1 < end_ && q_[l + 1].freq < q_[l].freq) l++;
-      if (x.freq <= q_[l].freq) break;
-      q_[i] = q_[l];
+    for (int l = 2; l < end; l = 2 * i) {
+      if (l + 1 < end && freq(q[l + 1]) < freq(q[l])) l++;
+      if (fx <= freq(q[l])) break;
+      q[i] = q[l];
       i = l;
     }
-    q_[i] = x;
+    q[i] = x;
     return top;
   }
-
-  int size() const { return end_ - 1; }
-  int32_t root() const { return q_[1].id; }
-
- private:
-  HeapEntry* q_;
-  int end_ = 1;
 };
 
+// Trees deeper than kLmax: lengthen the deepest non-maximal, rarest (then highest) symbol until
+// the Kraft sum fits.  The symbol picked stays the deepest after each step, so it is lengthened
+// until it reaches kLmax before another is picked, and the others keep their order: one sort
+// by (length desc, count asc, symbol desc), then a walk -- the same lengths as re-scanning for
+// the pick at every step (the oracle's limit_lengths, psz_oracle.c, does that).
 void limit_depth(const uint32_t* hist, int bklen, uint8_t* len)
 {
   const uint64_t full = 1ull << kLmax;
   uint64_t kraft = 0;
+  int cand[kMaxSym], nc = 0;
   for (int s = 0; s < bklen; s++)
     if (len[s]) {
       len[s] = std::min<uint8_t>(len[s], kLmax);
       kraft += 1ull << (kLmax - len[s]);
+      if (len[s] < kLmax) cand[nc++] = s;
     }
-  while (kraft > full) {  // lengthen the deepest non-maximal, rarest (then highest) symbol
-    int pick = -1;
-    for (int s = 0; s < bklen; s++) {
-      if (!len[s] || len[s] >= kLmax) continue;
-      if (pick < 0 || len[s] > len[pick] ||
-          (len[s] == len[pick] && (hist[s] < hist[pick] || (hist[s] == hist[pick] && s > pick))))
-        pick = s;
+  if (kraft <= full) return;
+  std::sort(cand, cand + nc, [&](int a, int b) {
+    if (len[a] != len[b]) return len[a] > len[b];
+    if (hist[a] != hist[b]) return hist[a] < hist[b];
+    return a > b;
+  });
+  for (int k = 0; k < nc && kraft > full; k++) {
+    const int s = cand[k];
+    while (kraft > full && len[s] < kLmax) {
+      kraft -= 1ull << (kLmax - len[s] - 1);
+      len[s]++;
     }
-    kraft -= 1ull << (kLmax - len[pick] - 1);
-    len[pick]++;
   }
 }
 
@@ -100,45 +104,38 @@ void limit_depth(const uint32_t* hist, int bklen, uint8_t* len)
 int huffman_code_lengths(const uint32_t* hist, int bklen, uint8_t* len)
 {
   std::memset(len, 0, bklen);
-  int used = 0, only = -1;
+  if (bklen > kMaxSym) return -1;
+  int16_t sym[kMaxSym];  // leaf id -> symbol (leaves 0..used-1 in symbol order)
+  int used = 0;
   for (int s = 0; s < bklen; s++)
-    if (hist[s]) used++, only = s;
+    if (hist[s]) sym[used++] = (int16_t)s;
   if (used == 0) return 0;
   if (used == 1) {
-    len[only] = 1;
+    len[sym[0]] = 1;
     return 1;
   }
-  // tree nodes: leaves 0..used-1, internal nodes after them (children ids)
-  thread_local std::vector<int32_t> kid;   // 2 per node
-  thread_local std::vector<int32_t> sym;   // leaf symbol
-  thread_local std::vector<HeapEntry> q;
-  thread_local std::vector<uint8_t> depth;
-  kid.resize(4 * (size_t)used), sym.resize(2 * (size_t)used), q.resize(2 * (size_t)used + 2), depth.resize(2 * (size_t)used);
-  MergeHeap heap(q.data());
-  int32_t nodes = 0;
-  for (int s = 0; s < bklen; s++)
-    if (hist[s]) {
-      sym[nodes] = s, kid[2 * nodes] = -1;
-      heap.push(hist[s], nodes++);
-    }
-  while (heap.size() > 1) {
-    const HeapEntry a = heap.pop(), b = heap.pop();
-    kid[2 * nodes] = a.id, kid[2 * nodes + 1] = b.id;
-    heap.push(a.freq + b.freq, nodes++);
+  MergeHeap heap;
+  for (int id = 0; id < used; id++) heap.push((uint64_t)hist[sym[id]] << kIdBits | (uint64_t)id);
+  // internal nodes after the leaves; parents are created after their children
+  int16_t parent[2 * kMaxSym];
+  int nodes = used;
+  const uint64_t idmask = (1ull << kIdBits) - 1;
+  while (heap.end > 2) {
+    const uint64_t a = heap.pop(), b = heap.pop();
+    parent[a & idmask] = (int16_t)nodes, parent[b & idmask] = (int16_t)nodes;
+    heap.push((MergeHeap::freq(a) + MergeHeap::freq(b)) << kIdBits | (uint64_t)nodes);
+    nodes++;
   }
-  // leaf depths: parents are created after their children, so a reverse sweep from the root
-  // sees every parent before its children
+  // depths by a reverse sweep from the root (every parent before its children)
+  uint8_t depth[2 * kMaxSym];
   int deepest = 0;
   depth[nodes - 1] = 0;
-  for (int32_t id = nodes - 1; id >= 0; id--) {
-    const int d = depth[id];
-    if (kid[2 * id] < 0) {
-      len[sym[id]] = (uint8_t)std::min(d, 255);
+  for (int id = nodes - 2; id >= 0; id--) {
+    const int d = std::min(depth[parent[id]] + 1, 255);
+    depth[id] = (uint8_t)d;
+    if (id < used) {
+      len[sym[id]] = (uint8_t)d;
       deepest = std::max(deepest, d);
-    }
-    else {
-      const int dc = std::min(d + 1, 255);
-      depth[kid[2 * id]] = (uint8_t)dc, depth[kid[2 * id + 1]] = (uint8_t)dc;
     }
   }
   if (deepest > kLmax) {

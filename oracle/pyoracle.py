@@ -253,14 +253,25 @@ def phf_segment(codes, bklen=1024, sublen=None, n_cu=256):
 
 
 # ------------------------------------------------------------------------ reference
+def _ref_outlier_cap(x, y, z):
+    """Outlier-list capacity for the reference CPU Lorenzo kernels: they predict every point of a
+    partial tile and append outliers with no bound check (lrz.seq.inl:266-284), so size by the
+    padded tile count (x to 256, y to 16, z to 8), as ref_shim.cc's StageRun does."""
+    up = lambda v, m: (v + m - 1) // m * m  # noqa: E731
+    ry = 1 if y == 1 else up(y, 16)
+    rz = 1 if z == 1 else up(z, 8)
+    return up(x, 256) + ry * x + rz * x * y
+
+
 def ref_lorenzo_c_f32(data, dims, eb, radius=512):
     data = np.ascontiguousarray(data, np.float32)
     x, y, z = dims
     n = x * y * z
     codes = np.zeros(n, np.uint16)
-    ov = np.zeros(n + 1, np.float32)
-    oi = np.zeros(n + 1, np.uint32)
-    k = ref().ref_c_lorenzo_f32(_ptr(data), x, y, z, eb, radius, _ptr(codes), _ptr(ov), _ptr(oi), n)
+    cap = _ref_outlier_cap(x, y, z)
+    ov = np.zeros(cap, np.float32)
+    oi = np.zeros(cap, np.uint32)
+    k = ref().ref_c_lorenzo_f32(_ptr(data), x, y, z, eb, radius, _ptr(codes), _ptr(ov), _ptr(oi), cap)
     return codes, ov[:k].copy(), oi[:k].copy()
 
 
@@ -270,9 +281,10 @@ def ref_lorenzo_c_zz_f32(data, dims, eb, radius=512):
     x, y, z = dims
     n = x * y * z
     codes = np.zeros(n, np.uint16)
-    ov = np.zeros(n + 1, np.float32)
-    oi = np.zeros(n + 1, np.uint32)
-    k = ref().ref_c_lorenzo_zz_f32(_ptr(data), x, y, z, eb, radius, _ptr(codes), _ptr(ov), _ptr(oi), n)
+    cap = _ref_outlier_cap(x, y, z)
+    ov = np.zeros(cap, np.float32)
+    oi = np.zeros(cap, np.uint32)
+    k = ref().ref_c_lorenzo_zz_f32(_ptr(data), x, y, z, eb, radius, _ptr(codes), _ptr(ov), _ptr(oi), cap)
     return codes, ov[:k].copy(), oi[:k].copy()
 
 
@@ -282,9 +294,10 @@ def ref_lorenzo3d_f64(data, dims, eb, radius=512):
     x, y, z = dims
     n = x * y * z
     codes = np.zeros(n, np.uint16)
-    ov = np.zeros(n + 1, np.float32)
-    oi = np.zeros(n + 1, np.uint32)
-    k = ref().ref_c_lorenzo3d_f64(_ptr(data), x, y, z, eb, radius, _ptr(codes), _ptr(ov), _ptr(oi), n)
+    cap = _ref_outlier_cap(x, y, z)
+    ov = np.zeros(cap, np.float32)
+    oi = np.zeros(cap, np.uint32)
+    k = ref().ref_c_lorenzo3d_f64(_ptr(data), x, y, z, eb, radius, _ptr(codes), _ptr(ov), _ptr(oi), cap)
     return codes, ov[:k].copy(), oi[:k].copy()
 
 

@@ -71,6 +71,31 @@ def test_ref_lorenzo3d_zigzag_f64_crosscheck(oracle, fixture, zigzag):
     np.testing.assert_array_equal(out, g["data"])
 
 
+@pytest.mark.parametrize("zigzag", [False, True])
+def test_ref_ragged_dense_outliers(oracle, zigzag):
+    """The compiled reference on a ragged field where almost every point is an outlier: its
+    outlier list is sized by the padded tile count (pyoracle._ref_outlier_cap), so partial-tile
+    appends past the field stay inside the buffer; the in-field part equals the oracle's."""
+    from oracle import pyoracle
+    if not pyoracle.ref_available():
+        pytest.skip("oracle/_ref not built (this container builds it from /root/reference)")
+    dims = (40, 24, 17)
+    rng = np.random.default_rng(11)
+    # integer data at eb = 0.5: the reference CPU kernel does not round, so only integer inputs
+    # make its quantization coincide with the oracle's (as in the crosschecks above)
+    data = rng.integers(-4000, 4000, size=dims[::-1]).astype(np.float32).ravel()
+    fn = pyoracle.ref_lorenzo_c_zz_f32 if zigzag else pyoracle.ref_lorenzo_c_f32
+    codes, ov, oi = fn(data, dims, 0.5)
+    n = data.size
+    assert len(oi) > n // 2
+    inside = oi < n
+    mine_codes, mine_ov, mine_oi = oracle.lorenzo_c(data, dims, eb=0.5, zigzag=zigzag)
+    order = np.argsort(oi[inside], kind="stable")
+    np.testing.assert_array_equal(mine_oi, oi[inside][order])
+    np.testing.assert_array_equal(mine_ov, ov[inside][order])
+    np.testing.assert_array_equal(mine_codes, codes)
+
+
 def test_ref_histogram(oracle):
     g = np.load(os.path.join(GOLDEN, "ref_hist.npz"))
     np.testing.assert_array_equal(oracle.histogram(g["codes"]), g["hist"])
