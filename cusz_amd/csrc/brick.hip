@@ -701,9 +701,8 @@ constexpr int pack_cells_words()
 {  // worst case cells of one row (27-bit codes) + slack, multiple of 4
   return ((64 * V * kLmax + 31) / 32 + 4 + 3) / 4 * 4;
 }
-constexpr int kPackRowMax = (64 * 4 * kLmax + 31) / 32 + 1;  // words one row's packing may touch
+constexpr int kPackRowMax = (64 * 4 * kLmax + 31) / 32 + 2;  // words one row's packing may touch
 constexpr int kPackCells = 768;  // per-wave LDS cell buffer (words): rows accumulate until a flush
-constexpr int kPackLdsWords = kMaxBklen + 256 + kBrickWaves * kPackCells;  // 19 KiB: 8 workgroups per CU
 static_assert(kPackCells >= 2 * kPackRowMax, "a flush every row or two at worst");
 
 // Pass 2 packs the brick's rows from the codes pass 1 left in brick order (row r of brick b at
@@ -712,21 +711,25 @@ static_assert(kPackCells >= 2 * kPackRowMax, "a flush every row or two at worst"
 // starts a new cell, hf_kernels.cuhip.inl:97-157).  Rows accumulate back to back in the buffer;
 // it is copied to the brick's region in coalesced 256-B stores when the next row might not fit
 // and at the brick's end.  Each row's load is issued when the same z of the previous y-step is
-// consumed (8 rows in flight).  About 60 VGPRs: 8 waves per SIMD, one brick per wave on a 512^3
-// field (no second round of waves).
+// consumed (8 rows in flight).  The loop is VALU-issue-bound (SQ counters: VALU busy ~75 % of
+// the kernel), so a row is kept to ~40 VALU: LDS tables at static addresses (their offsets fold
+// into the ds immediates), bricks inside the field take a path with no row checks, lanes pack
+// left-justified words with no exec masking, one lane records the row's size and entry in LDS.  ~60 VGPRs:
+// 8 waves per SIMD.
 template <int V, int ND>
-__global__ void __launch_bounds__(64 * kBrickWaves)
+__global__ void __launch_bounds__(64 * kBrickWaves) __attribute__((amdgpu_waves_per_eu(8)))
 k_brick3_pack(BrickCodes bcs, uint32_t ly, uint32_t lz, const uint32_t* __restrict__ book,
               int bklen, BrickPlanArgs pl, uint32_t* __restrict__ par_nbit, uint32_t* __restrict__ par_entry,
               uint32_t* __restrict__ bitstream, uint32_t nbx, uint32_t nby, uint32_t nbricks, int reverse,
               unsigned int* overflow, HostPub pub)
 {
   static_assert(V == 4, "8-B code loads");
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t* s_book = smem;             // kMaxBklen words: book word by code
-  uint32_t* s_b8 = smem + kMaxBklen;   // 256 words: book word by byte code (255: code 0)
+  __shared__ uint32_t s_book[kMaxBklen];  // book word by code
+  __shared__ uint32_t s_b8[256];          // book word by byte code (255: code 0)
+  __shared__ uint32_t s_cells[kBrickWaves][kPackCells];
+  __shared__ uint2 s_rowinfo[kBrickWaves][64];  // per row of the wave's brick: bits, first cell
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wid: uniform (SGPR)
-  uint32_t* cells = smem + kMaxBklen + 256 + wid * kPackCells;
+  uint32_t* const cells = s_cells[wid];
   const uint32_t nw = gridDim.x * kBrickWaves;  // (read before the divergent fill loops)
   for (int i = threadIdx.x; i < bklen; i += 64 * kBrickWaves) s_book[i] = book[i];
   for (int i = threadIdx.x; i < 256; i += 64 * kBrickWaves) {
@@ -745,10 +748,13 @@ k_brick3_pack(BrickCodes bcs, uint32_t ly, uint32_t lz, const uint32_t* __restri
     }
   }
   const uint32_t nunits = pl.nunits;
+  const uint32_t lo8 = (uint32_t)lane * 8u, lo4 = (uint32_t)lane * 4u;
   for (uint32_t it = blockIdx.x * kBrickWaves + wid; it < nunits; it += nw) {
     const uint32_t unit = reverse ? nunits - 1 - it : it;
     const uint32_t pb = unit / kPlanBricks;
-    const uint32_t base = pl.cell_local[unit] + pl.cell_pre[pb], lim = pl.ub[unit];
+    // (uniform values loaded per lane: read back as scalars)
+    const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)(pl.cell_local[unit] + pl.cell_pre[pb]));
+    const uint32_t lim = (uint32_t)__builtin_amdgcn_readfirstlane((int)pl.ub[unit]);
     {  // this unit's outlier slot -> the archive's outlier segment (unit = brick order)
       const uint32_t cnt = min(pl.brick_cnt[unit], pl.cap_per_brick);
       const uint64_t* slot = pl.slots + (size_t)unit * pl.cap_per_brick;
@@ -784,20 +790,24 @@ k_brick3_pack(BrickCodes bcs, uint32_t ly, uint32_t lz, const uint32_t* __restri
       // 1-D: rows [0, nrow) of the brick are chunks 64 brick + row (row = 8 y + z)
       const uint32_t nrow = ND == 1 ? min(64u, pl.nchunks - 64u * brick) : 64u;
       const uint32_t nyv = ND == 1 ? (nrow + 7u) / 8u : min(8u, ly - y0), nzv = ND == 1 ? 8u : min(8u, lz - z0);
-      auto row_ok = [&](uint32_t y, uint32_t z) { return ND == 1 ? y * 8u + z < nrow : z < nzv; };
-      const uint8_t* src16 = reinterpret_cast<const uint8_t*>(bcs.c16 + (size_t)brick * 64 * (64 * V)) + lane * 8;
-      const uint8_t* src8 = bcs.c8 + (size_t)brick * 64 * (64 * V) + lane * 4;
+      const uint8_t* src16 = reinterpret_cast<const uint8_t*>(bcs.c16 + (size_t)brick * 64 * (64 * V));
+      const uint8_t* src8 = bcs.c8 + (size_t)brick * 64 * (64 * V);
       const uint64_t rm = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bcs.rowmask[brick]) & 0xFFFFFFFFull) |
                           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(bcs.rowmask[brick] >> 32)) << 32);
       // row r: 8 u16 bytes per lane when bit r of rm is set, else 4 code bytes (.x); one 8-B load
-      // either way (a byte row's lane reads its neighbour's 4 bytes too: no branch around loads)
+      // either way (a byte row's lane reads its neighbour's 4 bytes too: no branch around loads);
+      // the row's base is uniform, the lane's offset one of two registers
       auto load_row = [&](uint32_t row) -> uint2 {
-        const uint8_t* a = (rm >> row) & 1ull ? src16 + (size_t)row * 512 : src8 + (size_t)row * 256;
+        const bool wide = (rm >> row) & 1ull;
+        const uint8_t* a = (wide ? src16 + (size_t)row * 512 : src8 + (size_t)row * 256) + (wide ? lo8 : lo4);
         uint2 v;
         __builtin_memcpy(&v, a, 8);
         return v;
       };
-      uint32_t my_nbit = 0, my_entry = 0;  // lane r: row r's bits and first cell
+      // full: every row of the brick lies in the field (no row checks, no short chunk)
+      const bool full = ND == 1 ? nrow == 64u && pl.n - (size_t)brick * 64u * (64u * V) >= 64u * 64u * V
+                                : nyv == 8u && nzv == 8u;
+      auto row_ok = [&](uint32_t y, uint32_t z) { return ND == 1 ? y * 8u + z < nrow : z < nzv; };
       // Straight-line row loop (no branch around a load: the compiler then waits for each row's
       // own load, not for all of them): every row's load is issued, rows outside the field read
       // a row of the brick's own code block and pack nothing.
@@ -819,17 +829,20 @@ k_brick3_pack(BrickCodes bcs, uint32_t ly, uint32_t lz, const uint32_t* __restri
             for (int k = 0; k < 4; k++) w[k] = s_b8[(qv[z].x >> (8 * k)) & 255u];
           }
           qv[z] = load_row((row + 8) & 63u);
-          if (!row_ok(y, z)) {
+          if (__builtin_expect(!full, 0)) {
+            asm volatile("" ::: "memory");  // a real branch: full bricks run no selects here
+            if (!row_ok(y, z)) {
 #pragma unroll
-            for (int k = 0; k < V; k++) w[k] = 0;
-          }
-          // 1-D: the field's last chunk may be short; codes past its end get no codeword
-          if (ND == 1) {
-            const size_t cfirst = ((size_t)brick * 64u + row) * (64u * V);
-            if (pl.n - cfirst < 64u * V)
+              for (int k = 0; k < V; k++) w[k] = 0;
+            }
+            // 1-D: the field's last chunk may be short; codes past its end get no codeword
+            if (ND == 1) {
+              const size_t cfirst = ((size_t)brick * 64u + row) * (64u * V);
+              if (pl.n - cfirst < 64u * V)
 #pragma unroll
-              for (int k = 0; k < V; k++)
-                if (cfirst + (uint32_t)lane * V + k >= pl.n) w[k] = 0;
+                for (int k = 0; k < V; k++)
+                  if (cfirst + (uint32_t)lane * V + k >= pl.n) w[k] = 0;
+            }
           }
           uint32_t bits = 0;
 #pragma unroll
@@ -838,20 +851,21 @@ k_brick3_pack(BrickCodes bcs, uint32_t ly, uint32_t lz, const uint32_t* __restri
           const uint32_t tot = readlane(inc, 63);
           const uint32_t pos = ((off - fbase) << 5) + inc - bits;
           if (__builtin_expect(__builtin_amdgcn_ballot_w64(bits > 64u) == 0, 1))
-            hfd::pack4_or(cells, pos, w, bits);
+            hfd::pack4_or_lj(cells, pos, w, bits);
           else
             hfd::pack_words<V>(cells, pos, w, V);
-          const uint32_t ent = base + off;
-          if ((uint32_t)lane == row) my_nbit = tot, my_entry = ent;
+          if (lane == 0) s_rowinfo[wid][row] = make_uint2(tot, base + off);  // the row's bits and first cell
           off += (tot + 31) >> 5;
         }
       }
-      flush();
+      flush();  // (ends with a wave sync: every row's info is in)
       const uint32_t ry = lane >> 3, rz = lane & 7;
-      if (row_ok(ry, rz) && ry < nyv) {
+      const bool lane_ok = ND == 1 ? (uint32_t)lane < nrow : ry < nyv && rz < nzv;
+      if (lane_ok) {
+        const uint2 ri = s_rowinfo[wid][lane];
         const size_t c = ND == 1 ? (size_t)brick * 64u + (uint32_t)lane : ((size_t)(z0 + rz) * ly + (y0 + ry)) * nbx + bx;
-        par_nbit[c] = my_nbit;
-        par_entry[c] = my_entry;
+        par_nbit[c] = ri.x;
+        par_entry[c] = ri.y;
       }
     }
     if (off > lim && lane == 0) atomicOr(overflow, 1u);  // cannot happen (region is an upper bound)
@@ -2496,7 +2510,7 @@ int brick_configure(BrickLaunch& L, int elem_bytes, int device)
   L.ncu = ncu;
   int per_scan = 0, per_pack = 0;
   const size_t lds_scan = (size_t)(1 + kBrickWaves * kHistCopies) * kMaxBklen * 4;
-  const size_t lds_pack = (size_t)kPackLdsWords * 4;
+  const size_t lds_pack = 0;  // static LDS only
   hipError_t e1, e2;
   if (elem_bytes == 8) {
     e1 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_scan, k_brick3_scan<double, 4, false>, 64 * kBrickWaves, lds_scan);
@@ -2567,7 +2581,7 @@ int launch_brick_pack(const BrickLaunch& L, const BrickCodes& bcodes, const uint
                       int reverse, unsigned int* overflow, hipStream_t st, const HostPub& pub)
 {
   const BrickGeom& g = L.g;
-  const size_t lds = (size_t)kPackLdsWords * 4;
+  const size_t lds = 0;  // static LDS only
   if (g.ndim != 3)
     k_brick3_pack<4, 1><<<L.grid_pack, 64 * kBrickWaves, lds, st>>>(bcodes, L.ly, L.lz, book, bklen, plan, par_nbit,
                                                                     par_entry, bitstream, g.nbx, g.nby, g.nbricks,

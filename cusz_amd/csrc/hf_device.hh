@@ -93,6 +93,28 @@ __device__ __forceinline__ void pack4_or(uint32_t* cells, uint32_t pos, const ui
   if (E >= 2) atomicOr(&cells[E - 2], w0);
 }
 
+// Same bits as pack4_or, addressed from the START of the lane's range: the <= 64 bits are
+// left-justified in hi:lo and OR-ed as the three words from word pos/32 on (bits past the lane's
+// range are 0, so the third word may be pure padding -- the caller keeps two words of zeroed
+// slack after the last row).  No exec masking: the shifts and alignbit take pos mod 32 from the
+// low bits of pos itself.  cells must be a compile-time LDS address (the word offsets fold into
+// the ds immediates).
+__device__ __forceinline__ void pack4_or_lj(uint32_t* cells, uint32_t pos, const uint32_t (&w)[4], uint32_t L)
+{
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    acc <<= (w[k] >> 27);
+    acc |= w[k] & 0x07FFFFFFu;
+  }
+  acc <<= (64u - L) & 63u;  // left-justify (L = 0: acc is 0 either way)
+  const uint32_t lo = (uint32_t)acc, hi = (uint32_t)(acc >> 32);
+  uint32_t* c = cells + (pos >> 5);
+  atomicOr(&c[0], hi >> (pos & 31u));
+  atomicOr(&c[1], __builtin_amdgcn_alignbit(hi, lo, pos & 31u));
+  atomicOr(&c[2], __builtin_amdgcn_alignbit(lo, 0u, pos & 31u));
+}
+
 // ---- decode tables --------------------------------------------------------------------------
 // Entry (u32) for the codeword(s) at the top of a window: [9:0] first symbol, [15:14] symbols
 // (1 or 2), [25:16] second symbol, [30:26] bits consumed, [31] two symbols.  0 = not in this
