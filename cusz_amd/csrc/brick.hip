@@ -38,6 +38,7 @@
 #include "hf_device.hh"
 #include "kernels.hh"
 #include "lrz_device.hh"
+#include "pub_device.hh"
 
 namespace cusz_amd {
 
@@ -206,27 +207,6 @@ __device__ __forceinline__ void store_brick_row(const BrickCodes& bcs, uint16_t*
     for (int k = 0; k < V; k++) w |= (qc[k] == 0 ? 255u : (uint32_t)qc[k] - bcs.c0) << (8 * k);
     *reinterpret_cast<uint32_t*>(cbrick8 + (size_t)row * (64 * V)) = w;
   }
-}
-
-// The workgroup that finishes last copies pub.r to the host and raises pub.flag.  The ticket is a
-// relaxed atomic taken after the workgroup's barrier (which waits for its memory operations,
-// atomics included): the last workgroup reads the words back by agent-scope atomic loads.  (An
-// agent-scope release per workgroup would write back the XCD's L2 each time.)
-__device__ __forceinline__ void publish_last(const HostPub& pub)
-{
-  if (!pub.flag) return;
-  __shared__ uint32_t s_last;
-  __syncthreads();
-  if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(pub.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return;
-  for (int k = 0; k < pub.r.count; k++)
-    for (int i = threadIdx.x; i < pub.r.nwords[k]; i += blockDim.x)
-      pub.r.dst[k][i] = __hip_atomic_load(pub.r.src[k] + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __threadfence_system();
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(pub.flag, pub.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // End of a pass-1 unit: outlier count, row mask, the unit's histogram as a u16 record (16-B
@@ -1461,7 +1441,7 @@ __device__ __forceinline__ void decode_chunks(const hfd::LdsTables<kDecB>& tb, c
 //    out of the entry with one or two instructions each;
 //  * the state is the position and the tile pointer: a lane takes part in a quarter while its
 //    pointer is below the block's limit and the ring holds every word the quarter can reach.
-// Smaller tables and tile (74 columns: 64 + the 9 overshoot) let 9 waves share a CU.
+// Smaller tables and tile (74 columns: 64 + the 9 overshoot) let up to 9 waves share a CU.
 constexpr int kTP4 = kBlk + 10;
 static_assert(((kTP4 / 2) & 1) == 1, "odd dword pitch");
 static_assert(kBlk + 2 * kF + 1 <= kTP4, "overshoot columns");
@@ -1470,8 +1450,10 @@ constexpr size_t kD4Tile = (size_t)(kRing4 + 2) * 256;          // slots 0..15, 
 constexpr size_t kD4Cells = kD4Tile + (size_t)64 * kTP4 * 2;
 constexpr size_t kD4Rows = kD4Cells + (size_t)kCellCap * 4;
 constexpr size_t kD4WaveBytes = kD4Rows + (size_t)(65 + 64) * 4;
+// 8 waves per CU: a 512^3 field's 8192 bricks are 4 full rounds of the 2048 waves (9 waves left
+// a partial fourth round: decode 285 -> 259 us)
 #ifndef CUSZ_AMD_DEC4_WAVES
-#define CUSZ_AMD_DEC4_WAVES 9
+#define CUSZ_AMD_DEC4_WAVES 8
 #endif
 #ifndef CUSZ_AMD_DEC4_REGWIN
 #define CUSZ_AMD_DEC4_REGWIN 0

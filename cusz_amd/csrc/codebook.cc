@@ -34,11 +34,8 @@ constexpr int kIdBits = 12;
 constexpr int kMaxSym = 1 << 10;  // bklen <= 1024 (kMaxBklen)
 
 struct MergeHeap {
-  // q[end] always holds a sentinel (maximal frequency): a missing right child never wins, so the
-  // sift-down picks the child without a branch
-  uint64_t q[2 * kMaxSym + 3];
+  uint64_t q[2 * kMaxSym + 2];
   int end = 1;
-  MergeHeap() { q[1] = ~0ull; }
 
   static uint64_t freq(uint64_t e) { return e >> kIdBits; }
 
@@ -46,7 +43,6 @@ struct MergeHeap {
   {
     const uint64_t f = freq(e);
     int i = end++;
-    q[end] = ~0ull;
     for (int j = i >> 1; j; j = i >> 1) {
       if (freq(q[j]) <= f) break;
       q[i] = q[j];
@@ -59,15 +55,12 @@ struct MergeHeap {
   {
     const uint64_t top = q[1];
     const uint64_t x = q[--end], fx = freq(x);
-    q[end] = ~0ull;
     int i = 1;
     for (int l = 2; l < end; l = 2 * i) {
-      const uint64_t a = q[l], b = q[l + 1];  // q[end] is the sentinel
-      const bool right = freq(b) < freq(a);
-      const uint64_t c = right ? b : a;
-      if (fx <= freq(c)) break;
-      q[i] = c;
-      i = l + (right ? 1 : 0);
+      if (l + 1 < end && freq(q[l + 1]) < freq(q[l])) l++;
+      if (fx <= freq(q[l])) break;
+      q[i] = q[l];
+      i = l;
     }
     q[i] = x;
     return top;

@@ -5,6 +5,22 @@
 
 namespace cusz_amd {
 
+struct XferRegions {
+  int count;
+  int nwords[4];
+  uint32_t* dst[4];
+  const uint32_t* src[4];
+};
+// Words the last workgroup of a kernel copies to the host before raising a host flag (the
+// kernel's own publish: no separate launch; pub_device.hh publish_last).  ticket: a word zeroed
+// before the launch.
+struct HostPub {
+  XferRegions r{};
+  uint32_t* flag = nullptr;  // null: no publish
+  uint32_t epoch = 0;
+  uint32_t* ticket = nullptr;
+};
+
 // Brick decomposition of the Lorenzo kernels (one wave64 per brick).
 struct LorenzoGeom {
   int ndim;
@@ -19,7 +35,7 @@ LorenzoGeom lorenzo_geom(int ndim, size_t lx, size_t ly, size_t lz, int elem_byt
 template <typename T>
 int launch_lorenzo_c(const T* in, size_t lx, size_t ly, size_t lz, double eb, int radius, bool zigzag,
                      const LorenzoGeom& g, uint16_t* codes, const OutlierSink& ol, uint32_t* hist,
-                     int bklen, hipStream_t st);
+                     int bklen, hipStream_t st, const HostPub& pub = HostPub{});
 
 // 1-D Lorenzo (non-ZigZag) reads the outlier values straight from the archive's cells when they
 // are in strictly increasing index order (this compressor's archives without spill): code 0 marks
@@ -122,16 +138,10 @@ struct OutlierCopyArgs {
   size_t bitstream_offset;  // byte offset of the bitstream (outliers follow it)
   const uint32_t* spill_start = nullptr;  // OutlierSink::spill_start (ranged spill) or nullptr
 };
-int launch_outlier_copy(const OutlierCopyArgs& a, hipStream_t st);
+int launch_outlier_copy(const OutlierCopyArgs& a, hipStream_t st, const HostPub& pub = HostPub{});
 
 
 // small host<->device transfers through host-mapped pinned memory (no stream sync)
-struct XferRegions {
-  int count;
-  int nwords[4];
-  uint32_t* dst[4];
-  const uint32_t* src[4];
-};
 int launch_publish(const XferRegions& r, uint32_t* flag, uint32_t epoch, hipStream_t st);
 int launch_upload(const XferRegions& r, hipStream_t st);
 // upload behind a device-polled host gate (the host sets *gate = epoch when the data is ready)
@@ -222,14 +232,6 @@ struct BrickCodes {
   uint8_t* c8;        // nbricks * 64 * W bytes
   uint64_t* rowmask;  // nbricks
   uint32_t c0;
-};
-// Words the last workgroup of a kernel copies to the host before raising a host flag (the
-// kernel's own publish: no separate launch).  ticket: a word zeroed before the launch.
-struct HostPub {
-  XferRegions r{};
-  uint32_t* flag = nullptr;  // null: no publish
-  uint32_t epoch = 0;
-  uint32_t* ticket = nullptr;
 };
 // pass 1: predict -> global + per-brick histograms, outliers, codes in brick order
 template <typename T>

@@ -17,6 +17,7 @@
 #include "common.hh"
 #include "kernels.hh"
 #include "lrz_device.hh"
+#include "pub_device.hh"
 
 namespace cusz_amd {
 
@@ -31,7 +32,7 @@ using namespace lrzd;
 template <typename T, bool ZZ>
 __global__ void __launch_bounds__(256)
 k_lorenzo_c1d(const T* __restrict__ in, size_t n, T ebx2_r, T r, uint16_t* __restrict__ codes,
-              OutlierSink ol, uint32_t* __restrict__ g_hist, int bklen, uint32_t nbricks)
+              OutlierSink ol, uint32_t* __restrict__ g_hist, int bklen, uint32_t nbricks, HostPub pub)
 {
   constexpr int V = 4;
   __shared__ uint32_t s_hist[kMaxBklen];
@@ -71,6 +72,7 @@ k_lorenzo_c1d(const T* __restrict__ in, size_t n, T ebx2_r, T r, uint16_t* __res
     if (lane == 0) ol.brick_cnt[brick] = cnt;
   }
   hist_flush(s_hist, g_hist, bklen);
+  publish_last(pub);  // the histogram to the host (pipeline.cc compress_scan)
 }
 
 // 2D: brick = (64V) x 32 rows (one tile row); tiles 32 wide.
@@ -78,7 +80,7 @@ template <typename T, int V, bool ZZ>
 __global__ void __launch_bounds__(256)
 k_lorenzo_c2d(const T* __restrict__ in, uint32_t lx, uint32_t ly, T ebx2_r, T r,
               uint16_t* __restrict__ codes, OutlierSink ol, uint32_t* __restrict__ g_hist, int bklen,
-              uint32_t nbx, uint32_t nbricks)
+              uint32_t nbx, uint32_t nbricks, HostPub pub)
 {
   __shared__ uint32_t s_hist[kMaxBklen];
   hist_init(s_hist, bklen);
@@ -113,6 +115,7 @@ k_lorenzo_c2d(const T* __restrict__ in, uint32_t lx, uint32_t ly, T ebx2_r, T r,
     if (lane == 0) ol.brick_cnt[brick] = cnt;
   }
   hist_flush(s_hist, g_hist, bklen);
+  publish_last(pub);  // the histogram to the host (pipeline.cc compress_scan)
 }
 
 // 3D: brick = (64V) x 8 x 8 (8V tiles of 8^3 along x).
@@ -120,7 +123,7 @@ template <typename T, int V, bool ZZ>
 __global__ void __launch_bounds__(256)
 k_lorenzo_c3d(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T ebx2_r, T r,
               uint16_t* __restrict__ codes, OutlierSink ol, uint32_t* __restrict__ g_hist, int bklen,
-              uint32_t nbx, uint32_t nby, uint32_t nbricks)
+              uint32_t nbx, uint32_t nby, uint32_t nbricks, HostPub pub)
 {
   __shared__ uint32_t s_hist[kMaxBklen];
   hist_init(s_hist, bklen);
@@ -173,6 +176,7 @@ k_lorenzo_c3d(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
     if (lane == 0) ol.brick_cnt[brick] = cnt;
   }
   hist_flush(s_hist, g_hist, bklen);
+  publish_last(pub);  // the histogram to the host (pipeline.cc compress_scan)
 }
 
 // =========================================================================================
@@ -559,28 +563,28 @@ LorenzoGeom lorenzo_geom(int ndim, size_t lx, size_t ly, size_t lz, int elem_byt
 template <typename T>
 int launch_lorenzo_c(const T* in, size_t lx, size_t ly, size_t lz, double eb, int radius, bool zigzag,
                      const LorenzoGeom& g, uint16_t* codes, const OutlierSink& ol, uint32_t* hist,
-                     int bklen, hipStream_t st)
+                     int bklen, hipStream_t st, const HostPub& pub)
 {
   const T ebx2_r = (T)(1.0 / (eb * 2));  // lrz_c.cuhip.inl:489
   const T r = (T)radius;
   const int grid = grid_for(g.nbricks);
   if (g.ndim == 1) {
     if (zigzag)
-      k_lorenzo_c1d<T, true><<<grid, 256, 0, st>>>(in, lx, ebx2_r, r, codes, ol, hist, bklen, g.nbricks);
+      k_lorenzo_c1d<T, true><<<grid, 256, 0, st>>>(in, lx, ebx2_r, r, codes, ol, hist, bklen, g.nbricks, pub);
     else
-      k_lorenzo_c1d<T, false><<<grid, 256, 0, st>>>(in, lx, ebx2_r, r, codes, ol, hist, bklen, g.nbricks);
+      k_lorenzo_c1d<T, false><<<grid, 256, 0, st>>>(in, lx, ebx2_r, r, codes, ol, hist, bklen, g.nbricks, pub);
   }
   else if (g.ndim == 2) {
     DISPATCH_V(g.V, if (zigzag) k_lorenzo_c2d<T, VV, true><<<grid, 256, 0, st>>>(
-                        in, lx, ly, ebx2_r, r, codes, ol, hist, bklen, g.nbx, g.nbricks);
+                        in, lx, ly, ebx2_r, r, codes, ol, hist, bklen, g.nbx, g.nbricks, pub);
                else k_lorenzo_c2d<T, VV, false><<<grid, 256, 0, st>>>(
-                   in, lx, ly, ebx2_r, r, codes, ol, hist, bklen, g.nbx, g.nbricks));
+                   in, lx, ly, ebx2_r, r, codes, ol, hist, bklen, g.nbx, g.nbricks, pub));
   }
   else {
     DISPATCH_V(g.V, if (zigzag) k_lorenzo_c3d<T, VV, true><<<grid, 256, 0, st>>>(
-                        in, lx, ly, lz, ebx2_r, r, codes, ol, hist, bklen, g.nbx, g.nby, g.nbricks);
+                        in, lx, ly, lz, ebx2_r, r, codes, ol, hist, bklen, g.nbx, g.nby, g.nbricks, pub);
                else k_lorenzo_c3d<T, VV, false><<<grid, 256, 0, st>>>(
-                   in, lx, ly, lz, ebx2_r, r, codes, ol, hist, bklen, g.nbx, g.nby, g.nbricks));
+                   in, lx, ly, lz, ebx2_r, r, codes, ol, hist, bklen, g.nbx, g.nby, g.nbricks, pub));
   }
   return (int)hipGetLastError();
 }
@@ -637,10 +641,10 @@ int launch_x1d_bounds(const uint32_t* cells, size_t ncell, size_t n, uint32_t nb
 
 template int launch_lorenzo_c<float>(const float*, size_t, size_t, size_t, double, int, bool,
                                      const LorenzoGeom&, uint16_t*, const OutlierSink&, uint32_t*, int,
-                                     hipStream_t);
+                                     hipStream_t, const HostPub&);
 template int launch_lorenzo_c<double>(const double*, size_t, size_t, size_t, double, int, bool,
                                       const LorenzoGeom&, uint16_t*, const OutlierSink&, uint32_t*, int,
-                                      hipStream_t);
+                                      hipStream_t, const HostPub&);
 template int launch_lorenzo_x<float>(const uint16_t*, float*, size_t, size_t, size_t, double, int, bool,
                                      const LorenzoGeom&, hipStream_t, const X1dOutliers*);
 template int launch_lorenzo_x<double>(const uint16_t*, double*, size_t, size_t, size_t, double, int, bool,

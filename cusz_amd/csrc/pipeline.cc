@@ -463,11 +463,18 @@ struct Pipeline {
                        reinterpret_cast<T*>(d_archive + 176),
                        ol,
                        d_hist};
+      pend.hist_epoch = 0;  // compress_finish publishes the histogram itself
       CUSZ_AMD_HIP_CHECK((hipError_t)launch_spline3_c<T>(sa, stream));
     }
     else {
+      // the kernel's last workgroup publishes the histogram to the host (no publish launch)
+      HostPub hp;
+      if (pub_hist)
+        hp = HostPub{regions({{h_hist(), d_hist, (size_t)bklen * 4}}), const_cast<uint32_t*>(flag(2)), ++epoch,
+                     reinterpret_cast<uint32_t*>(d_small + 24)};
+      pend.hist_epoch = hp.epoch;
       CUSZ_AMD_HIP_CHECK((hipError_t)launch_lorenzo_c<T>(in, len.x, len.y, len.z, eb, radius, zz, geom, d_codes,
-                                                         ol, d_hist, bklen, stream));
+                                                         ol, d_hist, bklen, stream, hp));
     }
     mark(2);
     pend.active = true;
@@ -497,16 +504,46 @@ struct Pipeline {
     const uint32_t cap = spl ? spl_cap : cap_per_brick;
     uint32_t* spill_start = spl ? d_spl_sps : nullptr;
 
-    // codebook on the host (hf_hl.cc:21-34), one round trip
-    int fs = fetch(hist_regions(bklen), 2);
-    if (fs) return fs;
-    const int rv = build_codebook(h_hist(), bklen, h_book(), h_revbook());
+    // codebook on the host (hf_hl.cc:21-34).  As in the brick path, every launch after the book
+    // is queued now behind a device-polled gate, and the last kernel publishes the summary: the
+    // histogram's trip to the host overlaps nothing, but no launch waits on the host's build.
+    uint32_t eh = pend.hist_epoch;  // published by the Lorenzo kernel's last workgroup, or now
+    if (!eh) {
+      eh = ++epoch;
+      CUSZ_AMD_HIP_CHECK((hipError_t)launch_publish(hist_regions(bklen), const_cast<uint32_t*>(flag(2)), eh, stream));
+    }
+    const uint32_t eg = ++gate_epoch;
+    const bool gated = gate;
+    struct GateGuard {  // the gate opens on every path out of here (see compress_brick)
+      volatile uint32_t* f;
+      uint32_t e;
+      bool armed;
+      ~GateGuard()
+      {
+        if (armed) __atomic_store_n(f, e, __ATOMIC_RELEASE);
+      }
+    } guard{flag(5), eg, gated};
+    auto build_book = [&]() -> int {
+      int fs = wait_flag(2, eh);
+      if (!fs) build_codebook(h_hist(), bklen, h_book(), h_revbook());
+      if (gated) __atomic_store_n(flag(5), eg, __ATOMIC_RELEASE);  // always open the gate
+      guard.armed = false;
+      return fs;
+    };
+    if (!gated)
+      if (int fs = build_book()) return fs;
     const size_t phf_off = 176 + anchor_bytes;  // anchors: spline only (compressor.inl:160)
-    const size_t rvbk = (size_t)rv;
+    const size_t rvbk = rvbk_bytes(bklen);
     const size_t nbit_rel = 128 + rvbk, entry_rel = nbit_rel + 4 * (size_t)pardeg;
     const size_t bits_rel = entry_rel + 4 * (size_t)pardeg;
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_upload(
-        regions({{d_book, h_book(), (size_t)bklen * 4}, {d_archive + phf_off + 128, h_revbook(), rvbk}}), stream));
+    {
+      const XferRegions up =
+          regions({{d_book, h_book(), (size_t)bklen * 4}, {d_archive + phf_off + 128, h_revbook(), rvbk}});
+      if (gated)
+        CUSZ_AMD_HIP_CHECK((hipError_t)launch_gate_upload(up, const_cast<const uint32_t*>(flag(5)), eg, timeout(), stream));
+      else
+        CUSZ_AMD_HIP_CHECK((hipError_t)launch_upload(up, stream));
+    }
     mark(3);
 
     HfEncodeArgs ea{d_codes,
@@ -542,8 +579,13 @@ struct Pipeline {
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_finalize_scan(fa, stream, h, &ph, d_archive, phf_off, bits_rel));
     OutlierCopyArgs oa{slots, bcnt,      boff,           nbr, cap, d_spill, spill_cnt(), spill_cap,
                        info(), d_archive, phf_off + bits_rel, spill_start};
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_outlier_copy(oa, stream));
+    // the copy's last workgroup publishes the summary finish_compress reads (no publish launch)
+    const HostPub sp{readback_regions(), const_cast<uint32_t*>(flag(3)), ++epoch, reinterpret_cast<uint32_t*>(d_small + 20)};
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_outlier_copy(oa, stream, sp));
+    summary_epoch = sp.epoch;
     mark(5);
+    if (gated)
+      if (int fs = build_book()) return fs;
     return finish_compress(h, out, outlen);
   }
 

@@ -8,6 +8,7 @@
 #include "archive_device.hh"
 #include "common.hh"
 #include "kernels.hh"
+#include "pub_device.hh"
 
 namespace cusz_amd {
 
@@ -114,15 +115,15 @@ __global__ void __launch_bounds__(1024) k_finalize_scan(FinalizeArgs a, HeaderTp
 }
 
 // one wave per brick copies its slot to the archive; trailing blocks copy the spill list
-__global__ void __launch_bounds__(256) k_outlier_copy(OutlierCopyArgs a, uint32_t spill_blocks)
+// (the last workgroup publishes the compress summary when pub.flag is set)
+__global__ void __launch_bounds__(256) k_outlier_copy(OutlierCopyArgs a, uint32_t spill_blocks, HostPub pub)
 {
   const unsigned long long ncell = a.info->total_ncell;
   uint32_t* dst = reinterpret_cast<uint32_t*>(a.archive + a.bitstream_offset + ncell * 4);
   const uint32_t slot_total = a.brick_off[a.nbricks];
   const uint32_t brick_blocks = gridDim.x - spill_blocks;
-  if (blockIdx.x < brick_blocks) {
-    const uint32_t brick = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (brick >= a.nbricks) return;
+  const uint32_t brick = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (blockIdx.x < brick_blocks && brick < a.nbricks) {
     const uint32_t all = a.brick_cnt[brick];
     const uint32_t cnt = min(all, a.cap_per_brick);
     const uint64_t* src = a.slots + (size_t)brick * a.cap_per_brick;
@@ -148,7 +149,7 @@ __global__ void __launch_bounds__(256) k_outlier_copy(OutlierCopyArgs a, uint32_
       }
     }
   }
-  else if (!a.spill_start) {
+  else if (blockIdx.x >= brick_blocks && !a.spill_start) {
     const uint32_t sp = min(*a.spill_cnt, a.spill_cap);
     uint32_t* d = dst + 2ull * slot_total;
     for (uint32_t i = (blockIdx.x - brick_blocks) * 256 + threadIdx.x; i < sp; i += spill_blocks * 256) {
@@ -157,6 +158,7 @@ __global__ void __launch_bounds__(256) k_outlier_copy(OutlierCopyArgs a, uint32_
       d[2 * i + 1] = (uint32_t)(c >> 32);
     }
   }
+  publish_last(pub);
 }
 
 template <typename T>
@@ -349,11 +351,11 @@ int launch_finalize_scan(const FinalizeArgs& a, hipStream_t st, const void* psz_
   return (int)hipGetLastError();
 }
 
-int launch_outlier_copy(const OutlierCopyArgs& a, hipStream_t st)
+int launch_outlier_copy(const OutlierCopyArgs& a, hipStream_t st, const HostPub& pub)
 {
   const uint32_t brick_blocks = (a.nbricks + 3) / 4;
   const uint32_t spill_blocks = 64;
-  k_outlier_copy<<<brick_blocks + spill_blocks, 256, 0, st>>>(a, spill_blocks);
+  k_outlier_copy<<<brick_blocks + spill_blocks, 256, 0, st>>>(a, spill_blocks, pub);
   return (int)hipGetLastError();
 }
 

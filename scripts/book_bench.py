@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Host codebook build time (cusz_amd/csrc/codebook.cc via tests/host/codebook_shim.cc, g++ -O3)
 on the config-2 histogram (tests/golden/config2_hist.npy: the oracle's codes of the 512^3 f32
-config-2 field at abs 1e-4, all 1024 symbols used).  Usage: python scripts/book_bench.py"""
+config-2 field at abs 1e-4, all 1024 symbols used).  Usage: python scripts/book_bench.py [codebook source]"""
 import ctypes as C
 import os
 import subprocess
@@ -14,11 +14,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def main():
+    import sys
+    src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "cusz_amd", "csrc", "codebook.cc")
     d = tempfile.mkdtemp()
     so = os.path.join(d, "libcb.so")
     subprocess.run(["g++", "-O3", "-std=c++17", "-shared", "-fPIC", "-o", so,
-                    os.path.join(ROOT, "tests", "host", "codebook_shim.cc"),
-                    os.path.join(ROOT, "cusz_amd", "csrc", "codebook.cc")], check=True)
+                    os.path.join(ROOT, "tests", "host", "codebook_shim.cc"), src], check=True)
     lib = C.CDLL(so)
     lib.shim_build_codebook.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
     h = np.load(os.path.join(ROOT, "tests", "golden", "config2_hist.npy")).astype(np.uint32)
@@ -31,7 +32,7 @@ def main():
     for _ in range(n):
         lib.shim_build_codebook(h.ctypes.data, 1024, book.ctypes.data, rv.ctypes.data)
     dt = (time.perf_counter() - t) / n
-    print(f"build_codebook (config-2 histogram, {int((h > 0).sum())} symbols): {dt * 1e6:.2f} us per call "
+    print(f"{os.path.basename(src)}: build_codebook (config-2 histogram, {int((h > 0).sum())} symbols): {dt * 1e6:.2f} us per call "
           f"(incl. ctypes call overhead)")
 
 
