@@ -12,7 +12,7 @@ struct XferRegions {
   const uint32_t* src[4];
 };
 // Words the last workgroup of a kernel copies to the host before raising a host flag (the
-// kernel's own publish: no separate launch; pub_device.hh publish_last).  ticket: a word zeroed
+// kernel's own publish: no separate launch; pub_device.hh publish_last).  ticket: 9 words zeroed
 // before the launch.
 struct HostPub {
   XferRegions r{};

@@ -147,6 +147,13 @@ struct Pipeline {
   unsigned int* ext_scratch() { return reinterpret_cast<unsigned int*>(d_small + 512); }
   uint32_t* dec_lut() { return reinterpret_cast<uint32_t*>(d_small + 512 + 2 * 1024 * 8); }
   static constexpr size_t kSmallBytes = 512 + 2 * 1024 * 8 + kHfDecScratchWords * 4;
+  // the publish tickets (9 words each, pub_device.hh); bytes [0, kSmallZeroBytes) are zeroed
+  // at the start of every compress
+  uint32_t* hist_ticket() { return reinterpret_cast<uint32_t*>(d_small + 160); }
+  uint32_t* summary_ticket() { return reinterpret_cast<uint32_t*>(d_small + 196); }
+  static constexpr size_t kSmallZeroBytes = 232;
+  static_assert(64 + sizeof(CompressInfo) <= 160 && 196 + 36 <= kSmallZeroBytes && kSmallZeroBytes <= 256,
+                "small-buffer layout");
 
   ~Pipeline() { release(); }
 
@@ -415,10 +422,10 @@ struct Pipeline {
     // per-call state reset (the reference never resets these: SURVEY.md Appendix B.3)
     if (brick)
       CUSZ_AMD_HIP_CHECK((hipError_t)launch_zero(
-          regions({{d_hist, nullptr, (size_t)(bklen + 1) * 4}, {d_small, nullptr, 64 + sizeof(CompressInfo)}}), stream));
+          regions({{d_hist, nullptr, (size_t)(bklen + 1) * 4}, {d_small, nullptr, kSmallZeroBytes}}), stream));
     else
       CUSZ_AMD_HIP_CHECK((hipError_t)launch_zero(regions({{d_hist, nullptr, (size_t)(bklen + 1) * 4},
-                                                          {d_small, nullptr, 64 + sizeof(CompressInfo)},
+                                                          {d_small, nullptr, kSmallZeroBytes},
                                                           {d_status, nullptr, status_words * 8}}),
                                                  stream));
     mark(1);
@@ -430,7 +437,7 @@ struct Pipeline {
       HostPub hp;
       if (pub_hist)
         hp = HostPub{regions({{h_hist(), d_hist, (size_t)bklen * 4}}), const_cast<uint32_t*>(flag(2)), ++epoch,
-                     reinterpret_cast<uint32_t*>(d_small + 24)};
+                     hist_ticket()};
       pend.hist_epoch = hp.epoch;
       CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_scan<T>(bl, in, eb, radius, zz, bol, d_hist, d_bhist,
                                                           brick_codes(zz, radius), bklen, stream, hp));
@@ -471,7 +478,7 @@ struct Pipeline {
       HostPub hp;
       if (pub_hist)
         hp = HostPub{regions({{h_hist(), d_hist, (size_t)bklen * 4}}), const_cast<uint32_t*>(flag(2)), ++epoch,
-                     reinterpret_cast<uint32_t*>(d_small + 24)};
+                     hist_ticket()};
       pend.hist_epoch = hp.epoch;
       CUSZ_AMD_HIP_CHECK((hipError_t)launch_lorenzo_c<T>(in, len.x, len.y, len.z, eb, radius, zz, geom, d_codes,
                                                          ol, d_hist, bklen, stream, hp));
@@ -580,8 +587,12 @@ struct Pipeline {
     OutlierCopyArgs oa{slots, bcnt,      boff,           nbr, cap, d_spill, spill_cnt(), spill_cap,
                        info(), d_archive, phf_off + bits_rel, spill_start};
     // the copy's last workgroup publishes the summary finish_compress reads (no publish launch)
-    const HostPub sp{readback_regions(), const_cast<uint32_t*>(flag(3)), ++epoch, reinterpret_cast<uint32_t*>(d_small + 20)};
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_outlier_copy(oa, stream, sp));
+    // when its grid is small; a large grid pays the publish per block, so a publish launch follows
+    const HostPub sp{readback_regions(), const_cast<uint32_t*>(flag(3)), ++epoch, summary_ticket()};
+    const bool in_copy = nbr <= 4096u;
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_outlier_copy(oa, stream, in_copy ? sp : HostPub{}));
+    if (!in_copy)
+      CUSZ_AMD_HIP_CHECK((hipError_t)launch_publish(sp.r, sp.flag, sp.epoch, stream));
     summary_epoch = sp.epoch;
     mark(5);
     if (gated)
@@ -669,7 +680,7 @@ struct Pipeline {
     pa.nd = g.ndim == 3 ? 3u : 1u, pa.nchunks = g.nchunks, pa.n = g.n;  // 1-D and 2-D: linear bricks
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_plan(bl, pa, h, &ph, stream));
     // the pack's last workgroup publishes the summary finish_compress reads (no publish launch)
-    const HostPub sp{readback_regions(), const_cast<uint32_t*>(flag(3)), ++epoch, reinterpret_cast<uint32_t*>(d_small + 20)};
+    const HostPub sp{readback_regions(), const_cast<uint32_t*>(flag(3)), ++epoch, summary_ticket()};
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_pack(bl, brick_codes(pend.zz, radius), d_book, bklen, pa, par_nbit, par_entry, bits,
                                                      pack_reverse, timeout(), stream, sp));
     summary_epoch = sp.epoch;
@@ -707,7 +718,7 @@ struct Pipeline {
     // look-back status words live in the per-brick histogram area (unused in this mode)
     unsigned long long* status = reinterpret_cast<unsigned long long*>(d_bhist);
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_zero(regions({{d_hist, nullptr, (size_t)bklen * 4},
-                                                        {d_small, nullptr, 64 + sizeof(CompressInfo)},
+                                                        {d_small, nullptr, kSmallZeroBytes},
                                                         {status, nullptr, (size_t)g.nbricks * 8}}),
                                                stream));
     mark(1);
@@ -750,7 +761,7 @@ struct Pipeline {
                    d_archive,
                    phf_off,
                    bits_rel};
-    const HostPub sp{readback_regions(), const_cast<uint32_t*>(flag(3)), ++epoch, reinterpret_cast<uint32_t*>(d_small + 20)};
+    const HostPub sp{readback_regions(), const_cast<uint32_t*>(flag(3)), ++epoch, summary_ticket()};
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_single<T>(bl, in, eb, radius, zz, sg, h, &ph, stream, sp));
     summary_epoch = sp.epoch;
     mark(4);

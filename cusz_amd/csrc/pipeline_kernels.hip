@@ -5,6 +5,8 @@
 // Reference counterparts: compress wrap-up psz/src/compressor.inl:398-418 (D2D concat),
 // phf header/offsets codec/hf/src/hf_buf.cc:191-211, GPU_extrema
 // psz/src/stat/detail/extrema.cuhip.inl:86-208.
+#include <algorithm>
+
 #include "archive_device.hh"
 #include "common.hh"
 #include "kernels.hh"
@@ -114,42 +116,45 @@ __global__ void __launch_bounds__(1024) k_finalize_scan(FinalizeArgs a, HeaderTp
   }
 }
 
-// one wave per brick copies its slot to the archive; trailing blocks copy the spill list
-// (the last workgroup publishes the compress summary when pub.flag is set)
+// one wave per brick copies its slot to the archive; trailing blocks copy the spill list.  The
+// last workgroup publishes the compress summary when pub.flag is set: that costs every block a
+// barrier on its stores and a ticket round trip, so the caller sets it only for small grids
+// (config 5's 16,448 blocks: 35 -> 196 us with it).
 __global__ void __launch_bounds__(256) k_outlier_copy(OutlierCopyArgs a, uint32_t spill_blocks, HostPub pub)
 {
   const unsigned long long ncell = a.info->total_ncell;
   uint32_t* dst = reinterpret_cast<uint32_t*>(a.archive + a.bitstream_offset + ncell * 4);
   const uint32_t slot_total = a.brick_off[a.nbricks];
   const uint32_t brick_blocks = gridDim.x - spill_blocks;
-  const uint32_t brick = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (blockIdx.x < brick_blocks && brick < a.nbricks) {
-    const uint32_t all = a.brick_cnt[brick];
-    const uint32_t cnt = min(all, a.cap_per_brick);
-    const uint64_t* src = a.slots + (size_t)brick * a.cap_per_brick;
-    uint32_t* d = dst + 2ull * a.brick_off[brick];
-    if ((reinterpret_cast<uintptr_t>(d) & 7) == 0) {  // the archive offset decides (wave-uniform)
-      uint64_t* d8 = reinterpret_cast<uint64_t*>(d);
+  if (blockIdx.x < brick_blocks) {
+    for (uint32_t brick = blockIdx.x * 4 + (threadIdx.x >> 6); brick < a.nbricks; brick += brick_blocks * 4) {
+      const uint32_t all = a.brick_cnt[brick];
+      const uint32_t cnt = min(all, a.cap_per_brick);
+      const uint64_t* src = a.slots + (size_t)brick * a.cap_per_brick;
+      uint32_t* d = dst + 2ull * a.brick_off[brick];
+      if ((reinterpret_cast<uintptr_t>(d) & 7) == 0) {  // the archive offset decides (wave-uniform)
+        uint64_t* d8 = reinterpret_cast<uint64_t*>(d);
 #pragma unroll 4
-      for (uint32_t i = threadIdx.x & 63; i < cnt; i += 64) d8[i] = src[i];
-    }
-    else
-#pragma unroll 4
-      for (uint32_t i = threadIdx.x & 63; i < cnt; i += 64) {
-        const uint64_t c = src[i];
-        d[2 * i] = (uint32_t)c;
-        d[2 * i + 1] = (uint32_t)(c >> 32);
+        for (uint32_t i = threadIdx.x & 63; i < cnt; i += 64) d8[i] = src[i];
       }
-    if (a.spill_start && all > cnt) {  // this brick's contiguous spill range follows its slot
-      const uint32_t s0 = a.spill_start[brick];
-      for (uint32_t i = threadIdx.x & 63; i < all - cnt; i += 64) {
-        const uint64_t c = s0 + i < a.spill_cap ? a.spill[s0 + i] : 0ull;
-        d[2 * (cnt + i)] = (uint32_t)c;
-        d[2 * (cnt + i) + 1] = (uint32_t)(c >> 32);
+      else
+#pragma unroll 4
+        for (uint32_t i = threadIdx.x & 63; i < cnt; i += 64) {
+          const uint64_t c = src[i];
+          d[2 * i] = (uint32_t)c;
+          d[2 * i + 1] = (uint32_t)(c >> 32);
+        }
+      if (a.spill_start && all > cnt) {  // this brick's contiguous spill range follows its slot
+        const uint32_t s0 = a.spill_start[brick];
+        for (uint32_t i = threadIdx.x & 63; i < all - cnt; i += 64) {
+          const uint64_t c = s0 + i < a.spill_cap ? a.spill[s0 + i] : 0ull;
+          d[2 * (cnt + i)] = (uint32_t)c;
+          d[2 * (cnt + i) + 1] = (uint32_t)(c >> 32);
+        }
       }
     }
   }
-  else if (blockIdx.x >= brick_blocks && !a.spill_start) {
+  else if (!a.spill_start) {
     const uint32_t sp = min(*a.spill_cnt, a.spill_cap);
     uint32_t* d = dst + 2ull * slot_total;
     for (uint32_t i = (blockIdx.x - brick_blocks) * 256 + threadIdx.x; i < sp; i += spill_blocks * 256) {
@@ -353,7 +358,7 @@ int launch_finalize_scan(const FinalizeArgs& a, hipStream_t st, const void* psz_
 
 int launch_outlier_copy(const OutlierCopyArgs& a, hipStream_t st, const HostPub& pub)
 {
-  const uint32_t brick_blocks = (a.nbricks + 3) / 4;
+  const uint32_t brick_blocks = std::max(1u, (a.nbricks + 3) / 4);
   const uint32_t spill_blocks = 64;
   k_outlier_copy<<<brick_blocks + spill_blocks, 256, 0, st>>>(a, spill_blocks, pub);
   return (int)hipGetLastError();

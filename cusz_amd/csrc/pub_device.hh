@@ -11,13 +11,26 @@ namespace cusz_amd {
 // atomics included): the last workgroup reads the words back by agent-scope atomic loads.  (An
 // agent-scope release per workgroup would write back the XCD's L2 each time.)  Every thread of
 // the workgroup must call it.
+// Two ticket levels (pub.ticket[0..7]: workgroups by blockIdx % 8; [8]: the groups' last ones):
+// one word takes at most ~90 returning atomics per µs, so a few thousand workgroups ending
+// together on one word would queue for tens of µs.
+constexpr uint32_t kPubGroups = 8;
+constexpr uint32_t kPubTicketWords = kPubGroups + 1;
+
 __device__ __forceinline__ void publish_last(const HostPub& pub)
 {
   if (!pub.flag) return;
   __shared__ uint32_t s_last;
   __syncthreads();
-  if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(pub.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  if (threadIdx.x == 0) {
+    const uint32_t n = gridDim.x, g = blockIdx.x % kPubGroups;
+    const uint32_t in_group = n / kPubGroups + (g < n % kPubGroups ? 1u : 0u);
+    const uint32_t groups = n < kPubGroups ? n : kPubGroups;
+    bool last = false;
+    if (__hip_atomic_fetch_add(pub.ticket + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_group - 1)
+      last = __hip_atomic_fetch_add(pub.ticket + kPubGroups, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == groups - 1;
+    s_last = last;
+  }
   __syncthreads();
   if (!s_last) return;
   for (int k = 0; k < pub.r.count; k++)

@@ -9,6 +9,10 @@ d=gpurun_out/pmc_$tag
 mkdir -p $d
 B="python3 bench.py --config $cfg --steps 5 --warmup 2 --profile-only --no-e2e $@"
 timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $d/stats -o run --output-format csv -- $B > $d/stats.log 2>&1 || exit 1
+# counter passes serialise dispatches, so a launch can block until the previous kernel ends: the
+# host could then never open the codebook gate the queued upload kernel polls.  Same kernels,
+# host-ordered upload instead (CUSZ_AMD_NO_GATE=1).
+export CUSZ_AMD_NO_GATE=1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $d/fetch -o run --output-format csv -- $B > $d/fetch.log 2>&1 || exit 1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $d/write -o run --output-format csv -- $B > $d/write.log 2>&1 || exit 1
 for x in stats fetch write; do
