@@ -571,9 +571,10 @@ k_brick1_scan(const T* __restrict__ in, size_t n, T ebx2_r, T r, OutlierSink ol,
 //  * block totals by agent-scope atomics; the block that finishes last scans them (every brick's
 //    base = local prefix + block prefix), fills the size fields and writes both headers.
 // Replaces the reference's host-side scans (hf_kernels.cuhip.inl:449-473, compressor.inl:398-418).
-constexpr int kPlanBricks = 64;  // units per plan block: 4 per wave, all loads issued together
+constexpr int kPlanBricks = 64;  // units per plan block: 4 per wave (one per wave, 512 blocks: 15 -> 20 us)
 constexpr int kPlanThreads = 1024;
 constexpr int kPlanWaves = kPlanThreads / 64;
+static_assert(kPlanBricks % kPlanWaves == 0 && kPlanBricks <= 64, "wave 0 scans the block's units");
 
 __device__ __forceinline__ uint32_t brick_rows3(uint32_t brick, uint32_t nbx, uint32_t nby, uint32_t ly, uint32_t lz)
 {
@@ -610,7 +611,7 @@ __global__ void __launch_bounds__(kPlanThreads) k_brick_plan(BrickPlanArgs a, He
         const int i = (k < 4 ? i0 : i1) + 2 * (k & 3);
         if (i < a.bhs) bits += (w[k] & 0xFFFFu) * s_len[i] + (w[k] >> 16) * s_len[i + 1];
       }
-      bits = hfd::wave_sum(bits);
+      bits = readlane(hfd::wave_incl_scan(bits), 63);  // DPP, no LDS round trips
       wbits += bits;
       uint32_t rows = 0;  // chunks of the unit: each may end with a partial cell
       for (uint32_t b = brick * kUnitBricks; b < min((brick + 1) * kUnitBricks, a.nbricks); b++)
@@ -622,20 +623,26 @@ __global__ void __launch_bounds__(kPlanThreads) k_brick_plan(BrickPlanArgs a, He
   }
   if (lane == 0) s_bits[wid] = wbits;
   __syncthreads();
-  if (wid == 0) {  // kPlanBricks == 64: one value per lane
-    const uint32_t ub = s_ub[lane], oc = s_oc[lane];
+  if (wid == 0) {  // one unit per lane (lanes < kPlanBricks)
+    const bool in = lane < kPlanBricks;
+    const uint32_t ub = in ? s_ub[lane] : 0u, oc = in ? s_oc[lane] : 0u;
     const uint32_t iu = hfd::wave_incl_scan(ub), io = hfd::wave_incl_scan(oc);
     const uint32_t brick = b0 + lane;
-    if (brick < a.nunits) a.ub[brick] = ub, a.cell_local[brick] = iu - ub, a.ol_local[brick] = io - oc;
+    if (in && brick < a.nunits) a.ub[brick] = ub, a.cell_local[brick] = iu - ub, a.ol_local[brick] = io - oc;
     if (lane == 63) {
       atomicExch(a.cell_pre + blockIdx.x, iu);
       atomicExch(a.ol_pre + blockIdx.x, io);
       unsigned long long tb = 0;
       for (int w = 0; w < kPlanWaves; w++) tb += s_bits[w];
       atomicAdd(&a.info->total_nbit, tb);
-      const uint32_t ticket =
-          __hip_atomic_fetch_add(&a.info->pad[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      s_last = ticket == nblk - 1;
+      // two-level ticket (pub_device.hh): blocks by blockIdx % 8, then the groups' last ones
+      const uint32_t g = blockIdx.x % kPubGroups;
+      const uint32_t in_group = nblk / kPubGroups + (g < nblk % kPubGroups ? 1u : 0u);
+      const uint32_t groups = nblk < kPubGroups ? nblk : kPubGroups;
+      bool last = false;
+      if (__hip_atomic_fetch_add(a.ticket + g, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == in_group - 1)
+        last = __hip_atomic_fetch_add(a.ticket + kPubGroups, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == groups - 1;
+      s_last = last;
     }
   }
   __syncthreads();

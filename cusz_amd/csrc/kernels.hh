@@ -256,12 +256,13 @@ struct BrickPlanArgs {
   uint32_t* ol_local;         // per brick: outlier offset inside its plan block
   uint32_t* cell_pre;         // nblk + 1: block prefixes, [nblk] = total cells
   uint32_t* ol_pre;           // nblk + 1: block prefixes, [nblk] = slot outliers
-  CompressInfo* info;         // totals; info->pad[0] = block ticket (zeroed per call)
+  CompressInfo* info;         // totals
   uint8_t* archive;
   size_t phf_offset, bitstream_rel;
   uint32_t nd = 3;       // 1: 1-D bricks (64 consecutive chunks; the last chunk may be short)
   uint32_t nchunks = 0;  // 1-D: chunks of the field
   size_t n = 0;          // 1-D: elements of the field
+  uint32_t* ticket = nullptr;  // 9 words zeroed per call: the two-level last-block ticket
 };
 uint32_t brick_units(uint32_t nbricks);
 uint32_t brick_plan_blocks(uint32_t nbricks);

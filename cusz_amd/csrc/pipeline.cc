@@ -151,8 +151,10 @@ struct Pipeline {
   // at the start of every compress
   uint32_t* hist_ticket() { return reinterpret_cast<uint32_t*>(d_small + 160); }
   uint32_t* summary_ticket() { return reinterpret_cast<uint32_t*>(d_small + 196); }
+  uint32_t* plan_ticket() { return reinterpret_cast<uint32_t*>(d_small + 112); }
   static constexpr size_t kSmallZeroBytes = 232;
-  static_assert(64 + sizeof(CompressInfo) <= 160 && 196 + 36 <= kSmallZeroBytes && kSmallZeroBytes <= 256,
+  static_assert(64 + sizeof(CompressInfo) <= 112 && 112 + 36 <= 160 && 196 + 36 <= kSmallZeroBytes &&
+                    kSmallZeroBytes <= 256,
                 "small-buffer layout");
 
   ~Pipeline() { release(); }
@@ -678,6 +680,7 @@ struct Pipeline {
                      d_brick_cnt, cap, d_slots, d_spill, spill_cnt(), spill_cap, nblk, d_ub, d_bbase, d_brick_off,
                      d_plan, d_plan + nblk + 1, info(), d_archive, phf_off, bits_rel};
     pa.nd = g.ndim == 3 ? 3u : 1u, pa.nchunks = g.nchunks, pa.n = g.n;  // 1-D and 2-D: linear bricks
+    pa.ticket = plan_ticket();
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_plan(bl, pa, h, &ph, stream));
     // the pack's last workgroup publishes the summary finish_compress reads (no publish launch)
     const HostPub sp{readback_regions(), const_cast<uint32_t*>(flag(3)), ++epoch, summary_ticket()};
