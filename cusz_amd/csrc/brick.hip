@@ -794,17 +794,22 @@ k_brick3_pack(BrickCodes bcs, uint32_t ly, uint32_t lz, const uint32_t* __restri
       // full: every row of the brick lies in the field (no row checks, no short chunk)
       const bool full = ND == 1 ? nrow == 64u && pl.n - (size_t)brick * 64u * (64u * V) >= 64u * 64u * V
                                 : nyv == 8u && nzv == 8u;
-      auto row_ok = [&](uint32_t y, uint32_t z) { return ND == 1 ? y * 8u + z < nrow : z < nzv; };
+      // Packing order: 3-D, the rows in order.  1-D, position k holds row 4 (k mod 16) + k / 16:
+      // the brick's 16 tiles' chunks of one phase are adjacent, as the 1-D decoder's lanes read
+      // them (lane = tile, phase p = the tile's chunk p: k_brick1_decode), so neighbouring lanes
+      // share cache lines instead of reading chunks 4 apart.  par_entry records the placement.
+      auto prow = [](uint32_t k) -> uint32_t { return ND == 1 ? 4u * (k & 15u) + (k >> 4) : k; };
+      auto row_ok = [&](uint32_t row) { return ND == 1 ? row < nrow : (row & 7u) < nzv; };
       // Straight-line row loop (no branch around a load: the compiler then waits for each row's
       // own load, not for all of them): every row's load is issued, rows outside the field read
       // a row of the brick's own code block and pack nothing.
       uint2 qv[8];
 #pragma unroll
-      for (int z = 0; z < 8; z++) qv[z] = load_row(z);
-      for (uint32_t y = 0; y < nyv; y++) {
+      for (int z = 0; z < 8; z++) qv[z] = load_row(prow(z));
+      for (uint32_t y = 0; y < (ND == 1 ? 8u : nyv); y++) {
 #pragma unroll
         for (int z = 0; z < 8; z++) {
-          const uint32_t row = y * 8 + z;
+          const uint32_t k = y * 8 + z, row = prow(k);
           if (off - fbase + kPackRowMax > kPackCells) flush();
           uint32_t w[V];
           if ((rm >> row) & 1ull) {
@@ -815,10 +820,10 @@ k_brick3_pack(BrickCodes bcs, uint32_t ly, uint32_t lz, const uint32_t* __restri
 #pragma unroll
             for (int k = 0; k < 4; k++) w[k] = s_b8[(qv[z].x >> (8 * k)) & 255u];
           }
-          qv[z] = load_row((row + 8) & 63u);
+          qv[z] = load_row(prow((k + 8) & 63u));
           if (__builtin_expect(!full, 0)) {
             asm volatile("" ::: "memory");  // a real branch: full bricks run no selects here
-            if (!row_ok(y, z)) {
+            if (!row_ok(row)) {
 #pragma unroll
               for (int k = 0; k < V; k++) w[k] = 0;
             }
