@@ -2097,21 +2097,22 @@ template <int DUMMY>
 __global__ void __launch_bounds__(64 * kDecWaves)
 k_chunk_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const uint8_t* __restrict__ revbook,
                int bklen, const uint32_t* __restrict__ par_nbit, const uint32_t* __restrict__ par_entry,
-               uint16_t* __restrict__ codes, size_t n, uint32_t nchunks, uint32_t sublen)
+               uint16_t* __restrict__ codes, size_t n, uint32_t nchunks, uint32_t sublen, uint32_t wpb)
 {
-  __shared__ hfd::LdsTables<kDecB> tb;
+  __shared__ hfd::Tab4 tb;
   extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
-  hfd::build_tables<kDecB>(tb, revbook, bklen);
-  const hfd::DecRegs rg = hfd::load_dec_regs(tb);
+  hfd::build_tab4(tb, revbook, bklen);
+  const hfd::DecRegs4 rg = hfd::load_dec_regs4(tb);
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* wbase = dsm + (size_t)wid * kDecRows;  // ring + tile (no cell staging)
-  uint16_t* tile = reinterpret_cast<uint16_t*>(wbase + kDecTile);
-  const DecWave dw{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(bitstream), 0, (int)(bs_words * 4u), (int)kBufRsrcW3),
-                   reinterpret_cast<uint32_t*>(wbase) + lane, tile, (uint32_t)bklen, lane};
-  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  uint8_t* wbase = dsm + (size_t)wid * kD4Cells;  // ring + tile (no cell staging)
+  uint16_t* tile = reinterpret_cast<uint16_t*>(wbase + kD4Tile);
+  const DecWave4 dw{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(bitstream), 0, (int)(bs_words * 4u), (int)kBufRsrcW3),
+                    reinterpret_cast<uint32_t*>(wbase) + lane, tile, (uint32_t)bklen, lane};
+  // waves [wpb, 8) only help build the tables (launch_chunk_decode)
+  const uint32_t nw = gridDim.x * wpb;
   const uint32_t nunits = (nchunks + 63) / 64;
   BPROF(unsigned long long pc[16] = {}; unsigned long long tk = __builtin_readcyclecounter(), tp = tk;)
-  for (uint32_t u = blockIdx.x * (blockDim.x >> 6) + wid; u < nunits; u += nw) {
+  for (uint32_t u = blockIdx.x * wpb + wid; (uint32_t)wid < wpb && u < nunits; u += nw) {
     const size_t c = (size_t)u * 64u + (uint32_t)lane;
     const bool live = c < nchunks;
     const uint32_t nbit = live ? par_nbit[c] : 0u;
@@ -2123,7 +2124,7 @@ k_chunk_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const 
 #pragma unroll 4
       for (uint32_t it = 0; it < 32; it++) {
         const uint32_t row = 2u * it + ((uint32_t)lane >> 5);
-        const uint32_t w = t32[row * (kTP / 2) + cp];
+        const uint32_t w = t32[row * (kTP4 / 2) + cp];
         const size_t e = ((size_t)u * 64u + row) * sublen + (uint32_t)blk * kBlk + 2u * cp;
         if ((uint32_t)blk * kBlk + 2u * cp >= sublen) continue;  // (sublen is a multiple of kBlk)
         if (e + 1 < n)
@@ -2132,7 +2133,7 @@ k_chunk_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const 
           codes[e] = (uint16_t)w;
       }
     };
-    decode_chunks(tb, rg, dw, live, vbase, nbit, vlen, [] {}, [](int) {}, recon BPROF_A, sublen);
+    decode_chunks4(tb, rg, dw, live, vbase, nbit, vlen, [] {}, [](int) {}, recon BPROF_A4, sublen, nullptr);
   }
 }
 
@@ -2716,11 +2717,16 @@ int launch_chunk_decode(const BrickLaunch& L, const uint32_t* bitstream, size_t 
   if (bs_words >= (1ull << 30) || bklen < 1 || bklen > kMaxBklen || sublen % kBlk != 0 || sublen == 0)
     return (int)hipErrorInvalidValue;
   if (!nchunks) return (int)hipSuccess;
-  const size_t lds = (size_t)kDecWaves * kDecRows;
+  // Fewer units than 8 per CU (a 2-D field of a few million values): spread them over every CU,
+  // ceil(units / nCU) decoding waves per workgroup, instead of 8 on a fifth of the chip; the
+  // workgroup keeps 8 waves so the tables take no longer to build.
   const uint32_t units = (nchunks + 63) / 64;
-  const uint32_t grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(L.ncu > 0 ? L.ncu : 256, (units + kDecWaves - 1) / kDecWaves));
+  const uint32_t ncu = L.ncu > 0 ? (uint32_t)L.ncu : 256u;
+  const uint32_t wpb = std::min<uint32_t>(kDecWaves, (units + ncu - 1) / ncu);
+  const size_t lds = (size_t)wpb * kD4Cells;
+  const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(ncu, (units + wpb - 1) / wpb));
   k_chunk_decode<0><<<grid, 64 * kDecWaves, lds, st>>>(bitstream, (uint32_t)bs_words, revbook, bklen, par_nbit,
-                                                       par_entry, codes, n, nchunks, sublen);
+                                                       par_entry, codes, n, nchunks, sublen, wpb);
   return (int)hipGetLastError();
 }
 

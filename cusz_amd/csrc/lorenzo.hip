@@ -23,6 +23,52 @@ namespace cusz_amd {
 
 using namespace lrzd;
 
+// Row loads by raw buffer instructions (2-D kernels): a row outside the field, or a lane past
+// its end, gets an offset past the row's range and reads 0, so the loads need no branch and the
+// waitcnt pass can count them (a load in a branch costs a wait for everything in flight).
+// The row's range is lx * sizeof(E) bytes: < 2^31 (launch_lorenzo_c / _x check).
+constexpr uint32_t kRowOOB = 0x80000000u;
+template <typename E>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const E* p, size_t row_start, uint32_t lx)
+{
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<E*>(p + row_start), 0, (int)(lx * sizeof(E)), 0x00020000);
+}
+template <typename T, int V>
+__device__ __forceinline__ void bload_row(__amdgpu_buffer_rsrc_t rs, uint32_t off, T (&v)[V])
+{
+  constexpr int B = (int)sizeof(T) * V;
+  if constexpr (B >= 16) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int h = 0; h < B / 16; h++) {
+      const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + 16u * h), 0, 0);
+      __builtin_memcpy(reinterpret_cast<char*>(&v[0]) + 16 * h, &w, 16);
+    }
+  }
+  else if constexpr (B == 8) {
+    const auto w = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)off, 0, 0);
+    __builtin_memcpy(&v[0], &w, 8);
+  }
+  else {
+    static_assert(B == 4, "row piece of 4, 8, 16 or 32 bytes");
+    const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 0);
+    __builtin_memcpy(&v[0], &w, 4);
+  }
+}
+// V codes packed two per u32
+template <int V>
+__device__ __forceinline__ void bload_codes(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t (&w)[(V + 1) / 2])
+{
+  if constexpr (V == 4) {
+    const auto q = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)off, 0, 0);
+    __builtin_memcpy(&w[0], &q, 8);
+  }
+  else if constexpr (V == 2)
+    w[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 0);
+  else
+    w[0] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rs, (int)off, 0, 0);
+}
+
 
 // =========================================================================================
 // predictor-quantizer kernels
@@ -93,15 +139,28 @@ k_lorenzo_c2d(const T* __restrict__ in, uint32_t lx, uint32_t ly, T ebx2_r, T r,
     T pprev[V];
 #pragma unroll
     for (int k = 0; k < V; k++) pprev[k] = 0;
+    // rows are loaded in groups of 8, a group ahead: a field of a few million values gives about
+    // one wave per SIMD, so a load per row would put 32 memory latencies in a row on every brick
+    constexpr int G = 8;
+    T raw[2][G][V];
+    auto issue = [&](int g) {
+#pragma unroll
+      for (int j = 0; j < G; j++) {
+        const uint32_t gy = y0 + g * G + j;
+        bload_row<T, V>(row_rsrc(in, (size_t)gy * lx, lx), gy < ly && x0 < lx ? x0 * (uint32_t)sizeof(T) : kRowOOB,
+                        raw[g & 1][j]);
+      }
+    };
+    issue(0);
+#pragma unroll
     for (int y = 0; y < 32; y++) {
       const uint32_t gy = y0 + y;
       const bool ok = gy < ly;
-      if (!__ballot(ok)) break;
       const size_t base = (size_t)gy * lx;
+      if (y % G == 0 && y + G < 32) issue(y / G + 1);
       T p[V];
-      load_row<T, V>(in, base, x0, lx, ok, p);
 #pragma unroll
-      for (int k = 0; k < V; k++) p[k] = dround(p[k] * ebx2_r);
+      for (int k = 0; k < V; k++) p[k] = dround(raw[(y / G) & 1][y % G][k] * ebx2_r);
       T a[V];
 #pragma unroll
       for (int k = 0; k < V; k++) a[k] = p[k] - pprev[k], pprev[k] = p[k];
@@ -373,13 +432,50 @@ k_lorenzo_x2d(const uint16_t* __restrict__ codes, T* out, uint32_t lx, uint32_t 
     const uint32_t bx = brick % nbx, by = brick / nbx;
     const uint32_t x0 = bx * (64 * V) + lane * V, y0 = by * 32;
     T s[V], S0[V], acc1[V], acc2[V];
+    // codes are loaded in groups of 8 rows, a group ahead (see k_lorenzo_c2d); a group with a
+    // zero code (an outlier) reads those values from the plane, in a branch that waits for them
+    constexpr int G = 8, W = (V + 1) / 2;
+    uint32_t cw[2][G][W];
+    auto issue = [&](int g) {
+#pragma unroll
+      for (int j = 0; j < G; j++) {
+        const uint32_t gy = y0 + g * G + j;
+        bload_codes<V>(row_rsrc(codes, (size_t)gy * lx, lx), gy < ly && x0 < lx ? x0 * 2u : kRowOOB, cw[g & 1][j]);
+      }
+    };
+    issue(0);
+    T val[G][V];  // the current group's values (o + c) - r
+#pragma unroll
     for (int y = 0; y < 32; y++) {
       const uint32_t gy = y0 + y;
       const bool ok = gy < ly;
-      if (!__ballot(ok)) break;
       const size_t base = (size_t)gy * lx;
+      if (y % G == 0) {
+        if (y + G < 32) issue(y / G + 1);
+        const int g = y / G;
+        bool anyz = false;
+#pragma unroll
+        for (int j = 0; j < G; j++)
+#pragma unroll
+          for (int k = 0; k < V; k++) {
+            const uint32_t c = (cw[g & 1][j][k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+            const bool in = y0 + g * G + j < ly && x0 + k < lx;
+            if constexpr (ZZ)
+              val[j][k] = in ? T(0) + (T)zz_dec((uint16_t)c) : T(0);
+            else
+              val[j][k] = in ? (T(0) + (T)c) - r : T(0);
+            anyz |= in && c == 0;
+          }
+        if (__ballot(anyz)) {
+#pragma unroll
+          for (int j = 0; j < G; j++)
+            fuse_codes<T, V, ZZ>(cw[g & 1][j], out, (size_t)(y0 + g * G + j) * lx, x0, lx, y0 + g * G + j < ly, r,
+                                 val[j]);
+        }
+      }
       T v[V];
-      fuse_row<T, V, ZZ>(codes, out, base, x0, lx, ok, r, v);
+#pragma unroll
+      for (int k = 0; k < V; k++) v[k] = val[y % G][k];
       const int strip = y >> 3;
       T t[V];
 #pragma unroll
@@ -575,6 +671,7 @@ int launch_lorenzo_c(const T* in, size_t lx, size_t ly, size_t lz, double eb, in
       k_lorenzo_c1d<T, false><<<grid, 256, 0, st>>>(in, lx, ebx2_r, r, codes, ol, hist, bklen, g.nbricks, pub);
   }
   else if (g.ndim == 2) {
+    if (lx * sizeof(T) >= 0x80000000ull) return (int)hipErrorInvalidValue;  // row_rsrc range
     DISPATCH_V(g.V, if (zigzag) k_lorenzo_c2d<T, VV, true><<<grid, 256, 0, st>>>(
                         in, lx, ly, ebx2_r, r, codes, ol, hist, bklen, g.nbx, g.nbricks, pub);
                else k_lorenzo_c2d<T, VV, false><<<grid, 256, 0, st>>>(
@@ -604,6 +701,7 @@ int launch_lorenzo_x(const uint16_t* codes, T* out, size_t lx, size_t ly, size_t
       k_lorenzo_x1d<T, false><<<grid, 256, 0, st>>>(codes, out, lx, ebx2, r, g.nbricks, o);
   }
   else if (g.ndim == 2) {
+    if (lx * sizeof(T) >= 0x80000000ull) return (int)hipErrorInvalidValue;  // row_rsrc range
     DISPATCH_V(g.V, if (zigzag) k_lorenzo_x2d<T, VV, true><<<grid, 256, 0, st>>>(
                         codes, out, lx, ly, ebx2, r, g.nbx, g.nbricks);
                else k_lorenzo_x2d<T, VV, false><<<grid, 256, 0, st>>>(codes, out, lx, ly, ebx2, r,
