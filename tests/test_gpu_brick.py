@@ -43,7 +43,7 @@ CASES = [
     ((50_000, 1, 1), np.float32, 1e-2, False, 512, "noise"),
     ((50_000, 1, 1), np.float32, 1e-3, False, 64, "hacc"),     # many outliers per block row
     ((40_000, 1, 1), np.float32, 0.5, False, 512, "int"),
-    # 2-D on linear bricks (x % 4 == 0, x >= 256): 2-D predictor, chunks in index order
+    # 2-D on linear bricks (x % 4 == 0, x >= 256): 2-D predictor, chunks as 1-D bricks place them
     ((3600, 90, 1), np.float32, 1e-4, False, 512, "cesm"),
     ((300, 97, 1), np.float32, 1e-4, False, 512, "cesm"),
     ((1024, 33, 1), np.float64, 1e-4, False, 512, "cesm"),
