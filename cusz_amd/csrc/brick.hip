@@ -1853,9 +1853,12 @@ k_brick1_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
       auto blk_start = [&](int blk) {
         if (blk == (int)(256 / kBlk) - 1) nxt = p < 3 ? fetch(u, p + 1) : fetch(u + nw, 0);
         if (!ranked) return;
+        // only pairs that start inside the chunk's cells: a chunk's cells are re-read by every
+        // block, and a phase's blocks lie too far apart for the lines to stay in L2
 #pragma unroll
         for (int h = 0; h < (int)kCellPf / 2; h++)
-          pf[h] = __builtin_amdgcn_raw_buffer_load_b128(rcells, (int)(live && npf ? cur * 8u + 16u * h : kOOB), 0, 0);
+          pf[h] = __builtin_amdgcn_raw_buffer_load_b128(
+              rcells, (int)(live && npf && cur + 2u * h < cend ? cur * 8u + 16u * h : kOOB), 0, 0);
       };
       auto recon = [&](int blk) {
 #ifdef CUSZ_AMD_EXP_NORECON
