@@ -2104,8 +2104,10 @@ k_chunk_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const 
 {
   __shared__ hfd::Tab4 tb;
   extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
+  BPROF(const unsigned long long tb0 = __builtin_readcyclecounter();)
   hfd::build_tab4(tb, revbook, bklen);
   const hfd::DecRegs4 rg = hfd::load_dec_regs4(tb);
+  BPROF(const unsigned long long tb1 = __builtin_readcyclecounter();)
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* wbase = dsm + (size_t)wid * kD4Cells;  // ring + tile (no cell staging)
   uint16_t* tile = reinterpret_cast<uint16_t*>(wbase + kD4Tile);
@@ -2136,8 +2138,16 @@ k_chunk_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const 
           codes[e] = (uint16_t)w;
       }
     };
+    BPROF(pc[0]++;)
     decode_chunks4(tb, rg, dw, live, vbase, nbit, vlen, [] {}, [](int) {}, recon BPROF_A4, sublen, nullptr);
   }
+#ifdef CUSZ_AMD_DEC_PROFILE
+  pc[11] += tb1 - tb0;  // table build (per wave)
+  pc[12] += __builtin_readcyclecounter() - tb0;  // whole wave
+  pc[13] += 1;
+  if (lane == 0)
+    for (int i = 0; i < 16; i++) atomicAdd(&g_brick_prof[i], pc[i]);
+#endif
 }
 
 
