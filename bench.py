@@ -237,18 +237,12 @@ def bench_field(args, world, rank, dist, dev):
         if not sharded:
             ptr, nb, _ = r.compress(x.data_ptr(), args.eb, mode)
             return ptr, nb
-        eb = args.eb
-        if mode == cz.Rel:  # r2r: eb times the whole field's value range (one all-reduce)
-            eb *= shard.global_value_ranges([r], [x], dist)[0]
-        for attempt in range(2):
-            r.compress_scan(x.data_ptr(), eb, hist.data_ptr())
-            shard.allreduce_histograms(hist, dist)  # RCCL, ordered on this stream: no host sync
-            try:
-                ptr, nb, _ = r.compress_finish(hist.data_ptr())
-                return ptr, nb
-            except cz.PszError as e:  # a slab overflowed its outlier capacity: all ranks repeat
-                if e.status != cz.PSZ_WARN_OUTLIER_TOO_MANY or attempt:
-                    raise
+        # pass 1 -> histogram all-reduce (RCCL, ordered on this stream: no host sync) -> finish;
+        # Rel mode: eb times the whole field's value range (one more all-reduce); a slab past its
+        # outlier capacity makes every rank repeat together (shard.compress_fields_sharded)
+        (ptr, nb), = shard.compress_fields_sharded([r], [x], args.eb, dist, mode=1 if mode == cz.Rel else 0,
+                                                   device=dev, hists=hist.view(1, -1))
+        return ptr, nb
 
     def step(acc=None, rot=True):
         if acc is not None:  # phase split: nothing of the previous step is still queued

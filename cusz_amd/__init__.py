@@ -107,7 +107,7 @@ EXPORTS = [
     # cusz_amd.h
     "psz_amd_get_internals", "psz_amd_enable_timing", "psz_amd_stage_times", "psz_amd_set_sublen",
     "psz_amd_decode_codes", "psz_amd_set_decoder", "psz_amd_set_layout", "psz_amd_set_codebook",
-    "psz_amd_version",
+    "psz_amd_version", "psz_amd_last_create_status",
     "psz_amd_compress_scan_float", "psz_amd_compress_scan_double", "psz_amd_compress_finish",
     "psz_amd_merge_archives", "psz_amd_value_range",
 ]

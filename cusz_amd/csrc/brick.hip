@@ -368,14 +368,10 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
               bool is_ol;
               qc[k] = quantize<T, ZZ>(d[k], r, is_ol, olv[k]);
               anyol |= __ballot(is_ol);
-#ifndef CUSZ_AMD_SCAN_NOHIST  // (timing experiment switch: no histogram)
               atomicAdd(&s_hist[qc[k] * kHistCopies + hc], 1u);
-#endif
             }
           }
-#ifndef CUSZ_AMD_SCAN_NOCODES  // (timing experiment switch: no code stores)
           store_brick_row<V>(bcs, cbrick, cbrick8, row, qc, rowmask);
-#endif
           if (anyol) {
             uint32_t mask = 0;
             size_t idx[V];
@@ -617,7 +613,9 @@ __global__ void __launch_bounds__(kPlanThreads) k_brick_plan(BrickPlanArgs a, He
       for (uint32_t b = brick * kUnitBricks; b < min((brick + 1) * kUnitBricks, a.nbricks); b++)
         rows += a.nd == 1 ? min(64u, a.nchunks - 64u * b) : brick_rows3(b, a.nbx, a.nby, a.ly, a.lz);
       ub = (bits + 31u * rows) >> 5;
-      oc = min(a.brick_cnt[brick], a.cap_per_brick);
+      const uint32_t bc = a.brick_cnt[brick];
+      oc = min(bc, a.cap_per_brick);
+      if (bc > a.cap_per_brick && lane == 0) atomicMax(&a.info->max_brick_cnt, bc);  // slot growth
     }
     if (lane == 0) s_ub[slot] = ub, s_oc[slot] = oc;
   }
@@ -676,6 +674,7 @@ __global__ void __launch_bounds__(kPlanThreads) k_brick_plan(BrickPlanArgs a, He
     a.info->total_ncell = ncell;
     a.info->splen = slot_total + sp_kept;
     a.info->outlier_lost = sp > a.spill_cap ? sp - a.spill_cap : 0u;
+    a.info->spilled = sp;
     write_headers_dev(a.archive, tpl, nbit, ncell, slot_total + sp_kept, a.phf_offset, a.bitstream_rel);
   }
 }
@@ -1750,9 +1749,6 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
     };
     auto recon = [&](int blk) {
       if (blk == (int)(W / kBlk) - 1) prefetch(nx);  // the next brick (fetched during this block)
-#ifdef CUSZ_AMD_EXP_NORECON3
-      if (blk < 100) return;
-#endif
       const uint32_t nyv = min(8u, ly - y0), nzv = min(8u, lz - z0);
       const size_t base_elem = (size_t)z0 * plane + (size_t)y0 * lx + (size_t)bx * W + (size_t)blk * kBlk;
       if (ranked)
@@ -1861,9 +1857,6 @@ k_brick1_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
               rcells, (int)(live && npf && cur + 2u * h < cend ? cur * 8u + 16u * h : kOOB), 0, 0);
       };
       auto recon = [&](int blk) {
-#ifdef CUSZ_AMD_EXP_NORECON
-        if (blk < 100) return;
-#endif
         const uint32_t roff = ((uint32_t)lane * 1024u + p * 256u + (uint32_t)blk * kBlk) * (uint32_t)sizeof(T);
         const uint32_t* trow = reinterpret_cast<const uint32_t*>(tile + lane * kTP4);
         if (ranked) {  // the prefetched values; ranks at or past the chunk's last cell read 0
@@ -1877,10 +1870,6 @@ k_brick1_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
         uint32_t tw[32];  // the row's 64 codes, all read before use (one LDS wait)
 #pragma unroll
         for (int q = 0; q < 32; q++) tw[q] = trow[q];
-#ifdef CUSZ_AMD_EXP_NOTW
-#pragma unroll
-        for (int q = 0; q < 32; q++) tw[q] = (uint32_t)(lane * 7 + q * 3 + blk) & 0x01FF01FFu;
-#endif
         uint32_t rk = 0;  // zero codes so far in this block
         // values of the codes: (o + c) - r, where a zero code's o is its cell by rank and any other
         // code's o is 0 -- one of the two is zero, so the sum is the other exactly and the value is
@@ -1898,11 +1887,7 @@ k_brick1_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
 #pragma unroll
               for (int e = 0; e < 16; e++) {
                 const uint32_t cd = (e & 1) ? tw[8 * s + e / 2] >> 16 : tw[8 * s + e / 2] & 0xFFFFu;
-#ifndef CUSZ_AMD_EXP_NOCV
                 val[e] = cv[rr];  // ranks past the prefetch: fixed below (reads stay in LDS)
-#else
-                val[e] = rr;
-#endif
                 rr += cd == 0u ? 1u : 0u;
               }
             }
@@ -1930,11 +1915,7 @@ k_brick1_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
           values(std::true_type{});
         else
           values(std::false_type{});
-#ifndef CUSZ_AMD_EXP_NOFAR
         if (ranked && __builtin_amdgcn_ballot_w64(rk > npf)) {  // ranks past the prefetch (rare)
-#else
-        if (false) {
-#endif
           uint32_t j = 0;
 #pragma unroll
           for (int q = 0; q < 32; q++) {
@@ -2383,6 +2364,7 @@ k_brick3_single(const T* __restrict__ in, SingleArgs a, T ebx2_r, T r)
     }
     if (lane == 0) {
       a.ol.brick_cnt[brick] = cnt;
+      if (cnt > a.ol.cap_per_brick) atomicMax(&a.info->max_brick_cnt, cnt);  // slot growth
       a.ol_pre[brick] = xo;
       atomicAdd(&a.info->total_nbit, bbits);
     }
@@ -2470,6 +2452,7 @@ __global__ void __launch_bounds__(256) k_brick3_single_finish(SingleArgs a, Head
     a.info->total_ncell = ncell;
     a.info->splen = slot_total + sp_kept;
     a.info->outlier_lost = sp > a.ol.spill_cap ? sp - a.ol.spill_cap : 0u;
+    a.info->spilled = sp;
     write_headers_dev(archive, tpl, nbit, ncell, slot_total + sp_kept, phf_offset, bits_rel);
     __threadfence();  // the header and totals reach memory before the ticket (the publisher may be another XCD)
   }

@@ -42,7 +42,9 @@ struct CompressInfo {
   unsigned long long splen;        // outlier cells written to the archive
   unsigned long long outlier_lost; // cells that did not fit (=> PSZ_WARN_OUTLIER_TOO_MANY)
   unsigned int lookback_timeout;   // nonzero if a bounded spin gave up (should never happen)
-  unsigned int pad[3];
+  unsigned int spilled;            // outlier cells past their brick's slot (the spill list)
+  unsigned int ticket;             // single-pass brick tickets
+  unsigned int max_brick_cnt;      // largest outlier count of one brick (slot growth)
 };
 
 }  // namespace cusz_amd

@@ -211,23 +211,37 @@ __device__ __forceinline__ uint16_t quantize(T d, T r, bool& ol, float& olval)
   }
 }
 
-// Rare path of emit_outliers: some cells of this row go past the brick's slot (out of line:
-// it must not bloat the unrolled hot loops).
+// Rare path of emit_outliers: some cells of this row go past the brick's slot.  The row's cells
+// past the slot take ONE reservation on the spill counter per wave (a ballot prefix gives each
+// lane its place): an outlier-dominated field (Nyx velocities at abs 1e-4) would otherwise issue
+// one returning atomic per element on a single word.  Called with the wave's active lanes of
+// emit_outliers (the whole row).
 template <int V>
 __device__ __forceinline__ void emit_outliers_spill(const OutlierSink& ol, uint32_t brick, uint32_t pos,
                                                               uint32_t mask, const float (&val)[V],
                                                               const size_t (&idx)[V])
 {
+  static_assert(V <= 15, "4 ballots count a lane's spilled cells");
   uint64_t* slot = ol.slots + (size_t)brick * ol.cap_per_brick;
+  const uint32_t cap = ol.cap_per_brick, c = (uint32_t)__popc(mask);
+  const uint32_t nsp = pos >= cap ? c : (pos + c > cap ? pos + c - cap : 0u);  // this lane's spilled cells
+  const uint64_t b0 = __ballot(nsp & 1u), b1 = __ballot(nsp & 2u), b2 = __ballot(nsp & 4u), b3 = __ballot(nsp & 8u);
+  const uint64_t lt = lanemask_lt();
+  const uint32_t excl = __popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt) + 8 * __popcll(b3 & lt);
+  const uint32_t tot = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2) + 8 * __popcll(b3);
+  const int leader = __ffsll((unsigned long long)__ballot(1)) - 1;
+  uint32_t s0 = 0;
+  if (lane_id() == leader) s0 = atomicAdd(ol.spill_cnt, tot);
+  uint32_t s = (uint32_t)__shfl((int)s0, leader) + excl;
 #pragma unroll
   for (int k = 0; k < V; k++) {
     if ((mask >> k) & 1u) {
       const uint64_t cell = make_cell(val[k], (uint32_t)idx[k]);
-      if (pos < ol.cap_per_brick)
+      if (pos < cap)
         slot[pos] = cell;
       else {
-        uint32_t s = atomicAdd(ol.spill_cnt, 1u);
         if (s < ol.spill_cap) ol.spill[s] = cell;
+        s++;
       }
       pos++;
     }

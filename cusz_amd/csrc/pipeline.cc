@@ -137,6 +137,7 @@ struct Pipeline {
   uint8_t* h_readback() const { return h_xfer + 64 + 8192 + 2560; }                            // 1 KB
 
   bool timing = false;
+  bool broken = false;  // an allocation failed mid-call (grow_spill): every later compress fails
   hipEvent_t ev[12] = {};
   float stage_ms[PSZ_AMD_T_COUNT] = {0};
 
@@ -181,12 +182,23 @@ struct Pipeline {
   }
 
   size_t rvbk_bytes(int bklen) const { return 4 * 64 + 2 * (size_t)bklen; }
-  // outlier slot per brick unit (brick.hip kUnitBricks bricks): 10 % of its elements + 16
-  uint32_t brick_cap() const
+  // outlier slot per brick unit (brick.hip kUnitBricks bricks): 10 % of its elements + 16 at
+  // first; a compress whose bricks spill grows it to the largest brick's count (grow_slots)
+  uint32_t brick_slot_cap = 0;
+  uint32_t brick_cap() const { return brick_slot_cap; }
+  uint32_t brick_unit_elems() const
   {
     const uint32_t nu = brick_units(bl.g.nbricks), per = (bl.g.nbricks + nu - 1) / nu;
-    return (uint32_t)((size_t)bl.g.brick_elems * per / 10 + 16);
+    return bl.g.brick_elems * per;
   }
+  // cells of every slot (reference-layout bricks and brick-layout units share d_slots)
+  size_t slot_cells_total() const
+  {
+    size_t c = (size_t)geom.nbricks * cap_per_brick;
+    if (bl.g.ok) c = std::max(c, (size_t)brick_units(bl.g.nbricks) * brick_slot_cap);
+    return c;
+  }
+  int grow_events = 0;  // capacity growths (a compress that warned repeats only after one)
 
   // fused brick path: 3-D, eligible shape, Lorenzo, default chunking (chunk = brick row)
   bool use_brick(psz_predictor pred) const
@@ -209,6 +221,9 @@ struct Pipeline {
     if (n >= (1ull << 32)) return PSZ_ABORT_UNSUPPORTED_DIMENSION;  // u32 outlier index (sp_interface.h)
     ndim = ndim_of(l);
     elem_bytes = dt == F8 ? 8 : 4;
+    // the 2-D Lorenzo kernels address one row through a 32-bit buffer range: a row of 2 GiB or
+    // more is a shape this build does not take (such a field compresses as 1-D)
+    if (ndim == 2 && l.x * (size_t)elem_bytes >= 0x80000000ull) return PSZ_ABORT_UNSUPPORTED_DIMENSION;
     stream = (hipStream_t)st;
     CUSZ_AMD_HIP_CHECK(hipGetDevice(&device));
     tune_chunking(n, device, &sublen, &pardeg);
@@ -228,11 +243,10 @@ struct Pipeline {
     spill_cap = (uint32_t)(n / 10 + 1024);
     bl.g = brick_geom(ndim, l.x, l.y, l.z, elem_bytes);
     bl.lx = (uint32_t)l.x, bl.ly = (uint32_t)l.y, bl.lz = (uint32_t)l.z;
-    size_t slot_cells = (size_t)geom.nbricks * cap_per_brick;
     uint32_t max_bricks = geom.nbricks;
     if (bl.g.ok) {
       CUSZ_AMD_HIP_CHECK((hipError_t)brick_configure(bl, elem_bytes, device));
-      slot_cells = std::max(slot_cells, (size_t)bl.g.nbricks * brick_cap());
+      brick_slot_cap = brick_unit_elems() / 10 + 16;
       max_bricks = std::max(max_bricks, bl.g.nbricks);
       CUSZ_AMD_HIP_CHECK(hipMalloc(&d_bhist, (size_t)bl.g.nbricks * kMaxBklen * sizeof(uint16_t)));
       CUSZ_AMD_HIP_CHECK(hipMalloc(&d_ub, (size_t)bl.g.nbricks * 4));
@@ -252,7 +266,7 @@ struct Pipeline {
     CUSZ_AMD_HIP_CHECK(hipMalloc(&d_codes, code_len * sizeof(uint16_t)));
     CUSZ_AMD_HIP_CHECK(hipMalloc(&d_hist, (kMaxBklen + 4) * sizeof(uint32_t)));  // + the sharded overflow word
     CUSZ_AMD_HIP_CHECK(hipMalloc(&d_book, kMaxBklen * sizeof(uint32_t)));
-    CUSZ_AMD_HIP_CHECK(hipMalloc(&d_slots, slot_cells * 8));
+    CUSZ_AMD_HIP_CHECK(hipMalloc(&d_slots, slot_cells_total() * 8));
     CUSZ_AMD_HIP_CHECK(hipMalloc(&d_brick_cnt, (size_t)max_bricks * 4));
     CUSZ_AMD_HIP_CHECK(hipMalloc(&d_brick_off, ((size_t)max_bricks + 1) * 4));
     CUSZ_AMD_HIP_CHECK(hipMalloc(&d_spill, (size_t)spill_cap * 8));
@@ -273,11 +287,51 @@ struct Pipeline {
   {
     const uint64_t cap = std::min<uint64_t>(need + need / 8 + 1024, (uint64_t)n + 1024);
     if (cap <= spill_cap) return 0;
+    // the new list is allocated before the old one is freed; on any failure the manager is marked
+    // broken (every later compress returns PSZ_AMD_ERR_DEVICE instead of handing a kernel a null
+    // list or archive)
+    uint64_t* grown = nullptr;
+    if (hipMalloc(&grown, cap * 8) != hipSuccess) {
+      broken = true;
+      return -1;
+    }
     (void)hipFree(d_spill);
-    d_spill = nullptr;
-    if (hipMalloc(&d_spill, cap * 8) != hipSuccess) return -1;
+    d_spill = grown;
     spill_cap = (uint32_t)cap;
-    return alloc_chunk_state() == hipSuccess ? 1 : -1;
+    if (alloc_chunk_state() != hipSuccess) {
+      broken = true;
+      return -1;
+    }
+    grow_events++;
+    return 1;
+  }
+
+  // Bricks with more outliers than their slot spilled to the shared list (archive valid, but the
+  // list's order depends on the atomics, so the archive is not deterministic and the decoders
+  // take the scatter path).  The slots of the layout just used grow to the largest brick's count
+  // (bounded by the brick's elements) and the caller repeats: identical below the 10 % slots.
+  // 1: grown, 0: already at the bound, -1: allocation failure (manager marked broken).
+  int grow_slots(uint32_t need)
+  {
+    const bool brick = last_layout == PSZ_AMD_LAYOUT_BRICK;
+    uint32_t& cap = brick ? brick_slot_cap : cap_per_brick;
+    const uint32_t lim = brick ? brick_unit_elems() : geom.brick_elems;
+    const uint32_t want = (uint32_t)std::min<uint64_t>(lim, (uint64_t)need + need / 8 + 16);
+    if (want <= cap) return 0;
+    cap = want;
+    uint64_t* grown = nullptr;
+    if (hipMalloc(&grown, slot_cells_total() * 8) != hipSuccess) {
+      broken = true;
+      return -1;
+    }
+    (void)hipFree(d_slots);
+    d_slots = grown;
+    if (alloc_chunk_state() != hipSuccess) {
+      broken = true;
+      return -1;
+    }
+    grow_events++;
+    return 1;
   }
 
   hipError_t alloc_chunk_state()
@@ -292,7 +346,7 @@ struct Pipeline {
     status_words = (size_t)hf_encode_groups(sublen, pardeg) + 1;
     hipError_t e = hipMalloc(&d_status, status_words * 8);
     if (e != hipSuccess) return e;
-    const size_t ol_cells = std::max((size_t)geom.nbricks * cap_per_brick, (size_t)sgeom.ntiles * spl_cap);
+    const size_t ol_cells = std::max(slot_cells_total(), (size_t)sgeom.ntiles * spl_cap);
     // chunk tables: the tuned chunking's, or the brick layout's (one chunk per brick row)
     const size_t chunks = std::max((size_t)pardeg, bl.g.ok ? (size_t)bl.g.nchunks : 0);
     archive_cap = 176 + (size_t)elem_bytes * sgeom.anchor_len + 128 + rvbk_bytes(kMaxBklen) + 8 * chunks +
@@ -355,9 +409,10 @@ struct Pipeline {
   template <typename T>
   int compress(psz_header* h, const T* in, uint8_t** out, size_t* outlen)
   {
+    if (broken) return PSZ_AMD_ERR_DEVICE;
     const psz_rc2 rc = h->rc;  // Rel mode scales eb in place: a second run starts from the caller's
     for (int run = 0;; run++) {
-      const uint32_t cap0 = spill_cap;
+      const int g0 = grow_events;
       int s;
       if (codebook == PSZ_AMD_CODEBOOK_SAMPLED && bl.g.ndim == 3 && use_brick(h->pipeline.predictor))
         s = compress_sampled<T>(h, in, out, outlen);
@@ -365,9 +420,9 @@ struct Pipeline {
         s = compress_scan<T>(h, in, true);
         if (!s) s = compress_finish(h, nullptr, out, outlen);
       }
-      // more outliers than the spill list held: it has grown to hold them all, compress again
-      // (identical below the reference's 10 % cap, where this never runs)
-      if (s != PSZ_WARN_OUTLIER_TOO_MANY || spill_cap == cap0 || run > 0) return s;
+      // bricks spilled past their slots (or past the spill list): the capacity has grown to hold
+      // them, compress again (identical below the reference's 10 % cap, where this never runs)
+      if (s != PSZ_WARN_OUTLIER_TOO_MANY || grow_events == g0 || run > 1) return s;
       h->rc = rc;
     }
   }
@@ -379,6 +434,7 @@ struct Pipeline {
   template <typename T>
   int compress_scan(psz_header* h, const T* in, bool pub_hist = false)
   {
+    if (broken) return PSZ_AMD_ERR_DEVICE;
     pend.active = false;
     pend.ext = false;
     const psz_predictor pred = h->pipeline.predictor;
@@ -702,6 +758,8 @@ struct Pipeline {
   int compress_sampled(psz_header* h, const T* in, uint8_t** out, size_t* outlen)
   {
     pend.active = false;
+    pend.ext = false;  // no caller's overflow word in this mode (finish_compress reads it when set)
+    pend.spl = false, pend.brick = true;
     if (h->pipeline.codec1 != Huffman) return PSZ_ABORT_NO_SUCH_CODEC;
     const bool zz = h->pipeline.predictor == LorenzoZigZag;
     const int radius = h->rc.radius, bklen = 2 * radius;
@@ -757,7 +815,7 @@ struct Pipeline {
                    reinterpret_cast<uint32_t*>(d_archive + phf_off + entry_rel),
                    reinterpret_cast<uint32_t*>(d_archive + phf_off + bits_rel),
                    status,
-                   &info()->pad[1],
+                   &info()->ticket,
                    d_ub,
                    info(),
                    timeout(),
@@ -809,12 +867,17 @@ struct Pipeline {
       stage_ms[PSZ_AMD_T_FINALIZE] = span(4, 5);
       stage_ms[PSZ_AMD_T_COMPRESS] = span(0, 5);
     }
-#ifdef CUSZ_AMD_DIAG_NOHIST  // diagnostic build: the reservation is knowingly wrong
-    tmo = 0;
-#endif
     if (tmo) {
       std::fprintf(stderr, "[cusz_amd] encoder reservation/look-back check failed\n");
       return PSZ_AMD_ERR_ENCODER;
+    }
+    if (ci.spilled && !pend.spl) {
+      // bricks spilled past their slots: grow the slots to the largest brick's count so that the
+      // repeat writes every cell in its brick's slot (deterministic order, fused decoders' ranked
+      // reads); compress() then runs once more, a scan/finish caller gets the warning and repeats
+      const int g = grow_slots(ci.max_brick_cnt);
+      if (g < 0) return PSZ_AMD_ERR_DEVICE;
+      if (g > 0) return PSZ_WARN_OUTLIER_TOO_MANY;
     }
     if (ci.outlier_lost) {
       // the spill list was too small for this field's outliers (every cell was counted): grow it
@@ -826,7 +889,9 @@ struct Pipeline {
     }
     // a sharded finish: another slab overflowed (the summed overflow word), so every rank sees
     // the warning and repeats the step together
-    if (global_excess()) return PSZ_WARN_OUTLIER_TOO_MANY;
+    const uint32_t gx = global_excess();
+    pend.ext = false;  // consumed: a later call never reads this finish's overflow word
+    if (gx) return PSZ_WARN_OUTLIER_TOO_MANY;
     *out = d_archive;
     *outlen = h->entry[PSZHEADER_ENC_PASS2_END];
     return PSZ_SUCCESS;
@@ -1001,8 +1066,11 @@ using cusz_amd::Pipeline;
 // resource-manager API (cusz_rev1.h)
 // =========================================================================================
 
+static thread_local int g_create_status = PSZ_SUCCESS;  // psz_amd_last_create_status
+
 static psz_resource* make_resource(psz_header* hdr, void* stream)
 {
+  g_create_status = PSZ_AMD_ERR_DEVICE;  // allocation failures below
   auto* m = new (std::nothrow) psz_resource;
   if (!m) return nullptr;
   std::memset(m, 0, sizeof(*m));
@@ -1017,6 +1085,7 @@ static psz_resource* make_resource(psz_header* hdr, void* stream)
     return nullptr;
   }
   int st = p->init(hdr->dtype, hdr->len, stream);
+  g_create_status = st;
   m->buf = p;
   m->ndim = p->ndim;
   m->last_error = (psz_error_status)st;
@@ -1033,7 +1102,9 @@ extern "C" {
 
 psz_resource* psz_create_resource_manager(psz_dtype dtype, psz_len len, psz_pipeline pipeline, void* stream)
 {
+  g_create_status = PSZ_ABORT_UNSUPPORTED_TYPE;
   if (dtype != F4 && dtype != F8) return nullptr;
+  g_create_status = PSZ_AMD_ERR_DEVICE;
   auto* h = new (std::nothrow) psz_header;
   if (!h) return nullptr;
   std::memset(h, 0, sizeof(*h));
@@ -1049,7 +1120,9 @@ psz_resource* psz_create_resource_manager(psz_dtype dtype, psz_len len, psz_pipe
 
 psz_resource* psz_create_resource_manager_from_header(psz_header* header, void* stream)
 {
+  g_create_status = !header ? PSZ_AMD_ERR_INVALID_ARG : PSZ_ABORT_UNSUPPORTED_TYPE;
   if (!header || (header->dtype != F4 && header->dtype != F8)) return nullptr;
+  g_create_status = PSZ_AMD_ERR_DEVICE;
   auto* h = new (std::nothrow) psz_header;
   if (!h) return nullptr;
   std::memcpy(h, header, sizeof(psz_header));
@@ -1121,8 +1194,11 @@ static int export_hist(psz_resource* m, uint32_t* d_out, int status)
   if (!d_out) return PSZ_AMD_ERR_INVALID_ARG;
   const int bklen = 2 * m->header->rc.radius;
   CUSZ_AMD_HIP_CHECK(hipMemcpyAsync(d_out, p->d_hist, sizeof(uint32_t) * bklen, hipMemcpyDeviceToDevice, p->stream));
-  // word bklen: this slab's outlier cells beyond its spill list (summed with the histograms)
-  CUSZ_AMD_HIP_CHECK((hipError_t)cusz_amd::launch_excess(p->spill_cnt(), p->spill_cap, d_out + bklen, p->stream));
+  // word bklen: this slab's spilled outlier cells -- past its bricks' slots (Lorenzo: every rank
+  // then repeats with grown slots, deterministic archives) or past its spill list (spline) --
+  // summed with the histograms
+  const uint32_t free_spill = p->pend.spl ? p->spill_cap : 0u;
+  CUSZ_AMD_HIP_CHECK((hipError_t)cusz_amd::launch_excess(p->spill_cnt(), free_spill, d_out + bklen, p->stream));
   return status;
 }
 
@@ -1310,6 +1386,8 @@ int psz_amd_decode_codes(psz_resource* m, uint8_t* in)
 }
 
 const char* psz_amd_version(void) { return "cusz_amd 0.1 (gfx950)"; }
+
+int psz_amd_last_create_status(void) { return g_create_status; }
 
 // internal: the older API passes a stream per call (cusz.h psz_compress/psz_decompress)
 int cusz_amd_set_stream(psz_resource* m, void* stream)

@@ -50,7 +50,7 @@ __global__ void __launch_bounds__(1024) k_finalize_scan(FinalizeArgs a, HeaderTp
   const uint32_t w0 = min((uint32_t)wid * seg, a.nbricks), w1 = min(w0 + seg, a.nbricks);
   const bool vec = (reinterpret_cast<uintptr_t>(a.brick_cnt) & 15) == 0;
   auto clamp = [&](uint32_t c) { return a.spill_start ? c : min(c, a.cap_per_brick); };
-  auto load4 = [&](uint32_t b) {  // counts b..b+3 of this segment (0 past its end)
+  auto load4raw = [&](uint32_t b) {  // counts b..b+3 of this segment (0 past its end)
     uint4 v{0, 0, 0, 0};
     if (vec && b + 3 < w1) v = *reinterpret_cast<const uint4*>(a.brick_cnt + b);
     else {
@@ -59,16 +59,22 @@ __global__ void __launch_bounds__(1024) k_finalize_scan(FinalizeArgs a, HeaderTp
       if (b + 2 < w1) v.z = a.brick_cnt[b + 2];
       if (b + 3 < w1) v.w = a.brick_cnt[b + 3];
     }
+    return v;
+  };
+  auto load4 = [&](uint32_t b) {
+    const uint4 v = load4raw(b);
     return uint4{clamp(v.x), clamp(v.y), clamp(v.z), clamp(v.w)};
   };
-  uint32_t sum = 0;
+  uint32_t sum = 0, mx = 0;  // mx: the largest count (the slot capacity a repeat needs)
 #pragma unroll 8
   for (uint32_t b = w0 + 4 * lane; b < w1; b += 256) {
-    const uint4 v = load4(b);
-    sum += v.x + v.y + v.z + v.w;
+    const uint4 v = load4raw(b);
+    mx = max(mx, max(max(v.x, v.y), max(v.z, v.w)));
+    sum += clamp(v.x) + clamp(v.y) + clamp(v.z) + clamp(v.w);
   }
 #pragma unroll
-  for (int d = 32; d > 0; d >>= 1) sum += __shfl_xor(sum, d);
+  for (int d = 32; d > 0; d >>= 1) sum += __shfl_xor(sum, d), mx = max(mx, (uint32_t)__shfl_xor((int)mx, d));
+  if (lane == 0 && mx) atomicMax(&a.info->max_brick_cnt, mx);
   if (lane == 0) s_scan[wid] = sum;
   __syncthreads();
   uint32_t carry = 0, total = 0;
@@ -111,6 +117,7 @@ __global__ void __launch_bounds__(1024) k_finalize_scan(FinalizeArgs a, HeaderTp
     a.info->total_ncell = ncell;
     a.info->splen = (unsigned long long)slot_total + (a.spill_start ? 0u : sp_kept);
     a.info->outlier_lost = sp > a.spill_cap ? sp - a.spill_cap : 0u;
+    a.info->spilled = sp;
     if (write_hdr)
       write_headers_dev(archive, hdr, a.info->total_nbit, ncell, a.info->splen, phf_offset, bitstream_rel);
   }

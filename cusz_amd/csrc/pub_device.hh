@@ -6,11 +6,12 @@
 
 namespace cusz_amd {
 
-// The workgroup that finishes last copies pub.r to the host and raises pub.flag.  The ticket is a
-// relaxed atomic taken after the workgroup's barrier (which waits for its memory operations,
-// atomics included): the last workgroup reads the words back by agent-scope atomic loads.  (An
-// agent-scope release per workgroup would write back the XCD's L2 each time.)  Every thread of
-// the workgroup must call it.
+// The workgroup that finishes last copies pub.r to the host and raises pub.flag.  Every wave first
+// waits for its own outstanding memory operations (s_waitcnt 0: the workgroup barrier alone does
+// not wait on vmcnt outside tgsplit mode, so another wave's no-return histogram atomics could
+// still be in flight), then the relaxed agent-scope ticket is taken after the barrier; the last
+// workgroup reads the words back by agent-scope atomic loads.  (An agent-scope release per
+// workgroup would write back the XCD's L2 each time.)  Every thread of the workgroup must call it.
 // Two ticket levels (pub.ticket[0..7]: workgroups by blockIdx % 8; [8]: the groups' last ones):
 // one word takes at most ~90 returning atomics per µs, so a few thousand workgroups ending
 // together on one word would queue for tens of µs.
@@ -21,6 +22,7 @@ __device__ __forceinline__ void publish_last(const HostPub& pub)
 {
   if (!pub.flag) return;
   __shared__ uint32_t s_last;
+  __builtin_amdgcn_s_waitcnt(0);  // this wave's stores and atomics have completed
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t n = gridDim.x, g = blockIdx.x % kPubGroups;

@@ -469,11 +469,7 @@ __global__ void __launch_bounds__(kSplThreads, 4) k_spline3_x(SplineXArgs<T> a)
     __syncthreads();
     // outlier codes of this tile and of the faces it shares with its upper neighbours: the
     // prefetched entries, then (rarely) the ones past kEnt * 256 straight from the buckets
-#ifdef CUSZ_AMD_DIAG_NOBUCKET  // diagnostic build: outliers ignored (wrong output)
-    if (false) {
-#else
     if (bk) {
-#endif
       uint32_t total = 0;
       for (int k = 0; k < 8; k++) total += s_rng[par][k][1] - s_rng[par][k][0];
 #pragma unroll

@@ -162,21 +162,35 @@ def compress_fields_sharded(resources, fields, eb, dist, mode=0, radius=512, dev
             r.compress_scan(t.data_ptr(), ebs[i], hists[i].data_ptr(), 0, radius)
         if dist is not None and dist.get_world_size() > 1:
             allreduce_histograms(hists, dist)  # the overflow words are summed with the counts
-        out, again = [], False
+        out, again, failure = [], False, None
         for i, r in enumerate(resources):
             try:
                 ptr, nb, _ = r.compress_finish(hists[i].data_ptr())
             except PszError as e:
                 # a slab had more outliers than its capacity (past the reference's 10 %): every
                 # rank sees it through the summed overflow word; the capacity has grown
-                if e.status != PSZ_WARN_OUTLIER_TOO_MANY or attempt:
-                    raise
-                again = True
+                if e.status == PSZ_WARN_OUTLIER_TOO_MANY and not attempt:
+                    again = True
+                    continue
+                failure = failure or e
+                # any other failure: when the summed overflow word makes the other ranks repeat,
+                # this rank repeats with them (their all-reduce would wait for it forever), then
+                # raises
+                if not attempt and retry_needed(hists[i], bklen):
+                    again = True
                 continue
             out.append((ptr, nb))
+        if failure is not None and not again:
+            raise failure
         if not again:
             return out
     return out
+
+
+def retry_needed(hist_row, bklen: int) -> bool:
+    """The summed overflow word of a reduced histogram row (u32[2 radius + 1]): nonzero when some
+    slab of this field overflowed its outlier list, so every rank repeats the scan."""
+    return int(hist_row[bklen].item()) != 0
 
 
 def merge(parts, full_dims, offsets=None) -> bytes:

@@ -144,6 +144,11 @@ int psz_amd_merge_archives(const uint8_t* const* parts, const size_t* part_bytes
 
 const char* psz_amd_version(void);
 
+/* Status of this thread's last psz_create_resource_manager* call (PSZ_SUCCESS when it returned a
+ * manager): the resource-manager API returns NULL on failure, as the reference does, and this
+ * says why -- e.g. PSZ_ABORT_UNSUPPORTED_DIMENSION for a shape the build does not take. */
+int psz_amd_last_create_status(void);
+
 #ifdef __cplusplus
 }
 #endif

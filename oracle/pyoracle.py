@@ -255,12 +255,21 @@ def phf_segment(codes, bklen=1024, sublen=None, n_cu=256):
 # ------------------------------------------------------------------------ reference
 def _ref_outlier_cap(x, y, z):
     """Outlier-list capacity for the reference CPU Lorenzo kernels: they predict every point of a
-    partial tile and append outliers with no bound check (lrz.seq.inl:266-284), so size by the
-    padded tile count (x to 256, y to 16, z to 8), as ref_shim.cc's StageRun does."""
+    partial tile and append outliers with no bound check (lrz.seq.inl:266-284), so the list holds
+    the padded tile volume (blocks of 256 / 16 x 16 / 8 x 8 x 8 by dimensionality; a count bound,
+    ref_shim.cc padded_points)."""
     up = lambda v, m: (v + m - 1) // m * m  # noqa: E731
-    ry = 1 if y == 1 else up(y, 16)
-    rz = 1 if z == 1 else up(z, 8)
-    return up(x, 256) + ry * x + rz * x * y
+    if z > 1:
+        return up(x, 8) * up(y, 8) * up(z, 8)
+    if y > 1:
+        return up(x, 16) * up(y, 16)
+    return up(x, 256)
+
+
+def _ref_count(k):
+    if k == 0xFFFFFFFF:
+        raise RuntimeError("reference CPU Lorenzo appended more outliers than the list holds")
+    return k
 
 
 def ref_lorenzo_c_f32(data, dims, eb, radius=512):
@@ -271,7 +280,7 @@ def ref_lorenzo_c_f32(data, dims, eb, radius=512):
     cap = _ref_outlier_cap(x, y, z)
     ov = np.zeros(cap, np.float32)
     oi = np.zeros(cap, np.uint32)
-    k = ref().ref_c_lorenzo_f32(_ptr(data), x, y, z, eb, radius, _ptr(codes), _ptr(ov), _ptr(oi), cap)
+    k = _ref_count(ref().ref_c_lorenzo_f32(_ptr(data), x, y, z, eb, radius, _ptr(codes), _ptr(ov), _ptr(oi), cap))
     return codes, ov[:k].copy(), oi[:k].copy()
 
 
@@ -284,7 +293,7 @@ def ref_lorenzo_c_zz_f32(data, dims, eb, radius=512):
     cap = _ref_outlier_cap(x, y, z)
     ov = np.zeros(cap, np.float32)
     oi = np.zeros(cap, np.uint32)
-    k = ref().ref_c_lorenzo_zz_f32(_ptr(data), x, y, z, eb, radius, _ptr(codes), _ptr(ov), _ptr(oi), cap)
+    k = _ref_count(ref().ref_c_lorenzo_zz_f32(_ptr(data), x, y, z, eb, radius, _ptr(codes), _ptr(ov), _ptr(oi), cap))
     return codes, ov[:k].copy(), oi[:k].copy()
 
 
@@ -297,7 +306,7 @@ def ref_lorenzo3d_f64(data, dims, eb, radius=512):
     cap = _ref_outlier_cap(x, y, z)
     ov = np.zeros(cap, np.float32)
     oi = np.zeros(cap, np.uint32)
-    k = ref().ref_c_lorenzo3d_f64(_ptr(data), x, y, z, eb, radius, _ptr(codes), _ptr(ov), _ptr(oi), cap)
+    k = _ref_count(ref().ref_c_lorenzo3d_f64(_ptr(data), x, y, z, eb, radius, _ptr(codes), _ptr(ov), _ptr(oi), cap))
     return codes, ov[:k].copy(), oi[:k].copy()
 
 

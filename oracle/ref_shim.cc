@@ -17,6 +17,7 @@
 //   phf_CPU_build_canonized_codebook_v2<u2,u4>                        codec/hf/src/hf_bk.seq.cc:72-145
 //   psz::module::CPU_scatter<f4,u4>::kernel_v2                        psz/src/kernel/spvn.seq.cc:19-29
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
@@ -41,14 +42,25 @@
 
 namespace {
 using Cell = _portable::compact_cell<f4, u4>;
+
+// Points the reference CPU Lorenzo kernels predict (and may append as outliers): every point of
+// every partial tile, i.e. the field padded to whole tiles of the dimension's block size
+// (lrz.seq.inl:154/250/354: 256, 16 x 16, 8 x 8 x 8).
+size_t padded_points(size_t x, size_t y, size_t z)
+{
+  auto up = [](size_t v, size_t m) { return (v + m - 1) / m * m; };
+  if (z > 1) return up(x, 8) * up(y, 8) * up(z, 8);
+  if (y > 1) return up(x, 16) * up(y, 16);
+  return up(x, 256);
 }
+}  // namespace
 
 extern "C" {
 
 // Reference CPU Lorenzo compress (NOT error-bounded: no round(); BLK 256/16/8).
 // Outliers are returned in the reference's sequential append order.
-// Returns the outlier count (capacity `ol_cap` must be >= N for safety: the
-// reference kernel does not bound-check).
+// Returns the outlier count, or UINT32_MAX when the kernel appended more than `ol_cap` cells (the
+// reference does not bound-check: size `ol_cap` by the padded tile volume, pyoracle does).
 uint32_t ref_c_lorenzo_f32(
     const float* in, size_t x, size_t y, size_t z, double eb, uint16_t radius, uint16_t* codes,
     float* ol_val, uint32_t* ol_idx, size_t ol_cap)
@@ -58,6 +70,7 @@ uint32_t ref_c_lorenzo_f32(
   psz::module::CPU_c_lorenzo_nd_with_outlier<f4, false, u2>::kernel(
       const_cast<float*>(in), len, codes, outlier.get(), eb, radius, nullptr);
   uint32_t n = outlier->num();
+  if (n > ol_cap) return UINT32_MAX;
   for (uint32_t i = 0; i < n; i++) {
     ol_val[i] = outlier->val_idx(i).val;
     ol_idx[i] = outlier->val_idx(i).idx;
@@ -75,6 +88,7 @@ uint32_t ref_c_lorenzo_zz_f32(
   psz::module::CPU_c_lorenzo_nd_with_outlier<f4, true, u2>::kernel(
       const_cast<float*>(in), len, codes, outlier.get(), eb, radius, nullptr);
   uint32_t n = outlier->num();
+  if (n > ol_cap) return UINT32_MAX;
   for (uint32_t i = 0; i < n; i++) {
     ol_val[i] = outlier->val_idx(i).val;
     ol_idx[i] = outlier->val_idx(i).idx;
@@ -94,6 +108,7 @@ uint32_t ref_c_lorenzo3d_f64(
   psz::KERNEL_SEQ_c_lorenzo_3d1l<f8, false, u2>(
       const_cast<double*>(in), len, leap3, radius, 1 / (eb * 2), codes, outlier.get());
   uint32_t n = outlier->num();
+  if (n > ol_cap) return UINT32_MAX;
   for (uint32_t i = 0; i < n; i++) {
     ol_val[i] = (float)outlier->val_idx(i).val;
     ol_idx[i] = outlier->val_idx(i).idx;
@@ -169,7 +184,8 @@ struct StageRun {
     npad = up(x, 256) + ry * x + rz * x * y;
     codes = std::make_unique<uint16_t[]>(n);
     memset(codes.get(), 0, sizeof(uint16_t) * n);  // pages faulted in before the clocks
-    outlier = std::make_unique<_portable::compact_CPU<f4, u4>>(npad);
+    // the outlier list holds every predicted point (a count bound, unlike npad's index bound)
+    outlier = std::make_unique<_portable::compact_CPU<f4, u4>>(std::max(npad, padded_points(x, y, z)));
     hist = std::make_unique<uint32_t[]>(2 * radius);
     book = std::make_unique<uint32_t[]>(2 * radius);
     rvbk_bytes = (int)phf_reverse_book_bytes(2 * radius, 4, sizeof(u2));

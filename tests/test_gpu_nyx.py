@@ -20,7 +20,11 @@ FULL = (512, 512, 512)
 WORLD = 8
 
 
-def test_nyx_six_fields_sharded_equals_whole():
+@pytest.mark.parametrize("bound", ["r2r", "abs"])
+def test_nyx_six_fields_sharded_equals_whole(bound):
+    """r2r 1e-4 (the reference's runtests bound) and abs 1e-4 (SURVEY §8d's config-4 bound: the
+    velocity fields are mostly outliers, far past the 10 % slots; the slots grow to the largest
+    brick's count, so every cell stays in its brick's slot and the merge is still byte-exact)."""
     slabs = shard.plan_slabs(FULL, WORLD)
     assert [s.dims[2] for s in slabs] == [64] * WORLD
     st = torch.cuda.current_stream().cuda_stream
@@ -39,25 +43,35 @@ def test_nyx_six_fields_sharded_equals_whole():
         sync()
         lo, hi = mm[:, 0].min().item(), mm[:, 1].max().item()
         assert lo == f.min().item() and hi == f.max().item()
-        eb = r2r * (hi - lo)
-        for k, (r, v) in enumerate(zip(res, views)):
-            r.compress_scan(v.data_ptr(), eb, hists[k].data_ptr())
-        sync()
-        g = hists.to(torch.int64).sum(0)
-        assert int(g[:1024].sum().item()) == f.numel() and int(g[1024].item()) == 0
-        g32 = g.to(torch.int32).contiguous()
-        parts = []
-        for r in res:
-            ptr, nb, _ = r.compress_finish(g32.data_ptr())
-            parts.append(d2h(ptr, nb).tobytes())
+        eb = r2r * (hi - lo) if bound == "r2r" else 1e-4
+        for attempt in range(2):  # a slab past its slots: every slab repeats once (shard.py)
+            for k, (r, v) in enumerate(zip(res, views)):
+                r.compress_scan(v.data_ptr(), eb, hists[k].data_ptr())
+            sync()
+            g = hists.to(torch.int64).sum(0)
+            assert int(g[:1024].sum().item()) == f.numel()
+            assert attempt == 0 or int(g[1024].item()) == 0
+            g32 = g.to(torch.int32).contiguous()
+            parts, again = [], False
+            for r in res:
+                try:
+                    ptr, nb, _ = r.compress_finish(g32.data_ptr())
+                except cz.PszError as e:
+                    assert e.status == cz.PSZ_WARN_OUTLIER_TOO_MANY and attempt == 0
+                    again = True
+                    continue
+                parts.append(d2h(ptr, nb).tobytes())
+            if not again:
+                break
+        assert len(parts) == WORLD
         merged = shard.merge(parts, FULL, [s.offset for s in slabs])
         ptr, nb, _ = whole.compress(f.data_ptr(), eb, cz.Abs)
         single = d2h(ptr, nb).tobytes()
         assert len(merged) == len(single), fi
         assert merged == single, f"field {fi}: merged archive differs from the whole-field archive"
-        # Rel mode on the whole field finds the same absolute bound
-        whole.compress(f.data_ptr(), r2r, cz.Rel)
-        assert whole.header.rc.eb == eb
+        if bound == "r2r":  # Rel mode on the whole field finds the same absolute bound
+            whole.compress(f.data_ptr(), r2r, cz.Rel)
+            assert whole.header.rc.eb == eb
         # the merged archive decompresses within the bound
         d_arch = torch.frombuffer(bytearray(merged), dtype=torch.uint8).cuda()
         hdr = cz.psz_header.from_buffer_copy(merged[:176])
