@@ -107,7 +107,7 @@ EXPORTS = [
     # cusz_amd.h
     "psz_amd_get_internals", "psz_amd_enable_timing", "psz_amd_stage_times", "psz_amd_set_sublen",
     "psz_amd_decode_codes", "psz_amd_set_decoder", "psz_amd_set_layout", "psz_amd_set_codebook",
-    "psz_amd_version", "psz_amd_last_create_status",
+    "psz_amd_version", "psz_amd_last_create_status", "psz_amd_build_book_device",
     "psz_amd_compress_scan_float", "psz_amd_compress_scan_double", "psz_amd_compress_finish",
     "psz_amd_merge_archives", "psz_amd_value_range",
 ]
@@ -165,6 +165,9 @@ def lib():
     L.psz_amd_merge_archives.argtypes = [C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.c_int,
                                          C.POINTER(C.c_size_t), psz_len, P, C.c_size_t,
                                          C.POINTER(C.c_size_t)]
+    L.psz_amd_build_book_device.restype = C.c_int
+    L.psz_amd_build_book_device.argtypes = [P, C.c_int, C.c_uint32, P, P, P]
+    L.psz_amd_last_create_status.restype = C.c_int
     L.phf_coarse_tune.argtypes = [C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.pszheader_filesize.restype = C.c_size_t
     L.pszheader_filesize.argtypes = [C.POINTER(psz_header)]
@@ -306,6 +309,15 @@ class Resource:
 
 
 _hip = None
+
+
+def build_book_device(d_hist: int, bklen: int, smooth: int, d_book: int, d_revbook: int, stream: int = 0) -> None:
+    """The device codebook (psz_amd_build_book_device): device u32[bklen] histogram (+ smooth per
+    bin) -> device book u32[bklen] and reverse book (4 * 64 + 2 * bklen bytes), on `stream`."""
+    st = lib().psz_amd_build_book_device(C.c_void_p(d_hist), bklen, smooth, C.c_void_p(d_book),
+                                         C.c_void_p(d_revbook), C.c_void_p(stream))
+    if st != 0:
+        raise PszError(st, "psz_amd_build_book_device")
 
 
 def hip_memcpy(dst: int, src: int, nbytes: int, kind: int) -> None:

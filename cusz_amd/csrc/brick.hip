@@ -34,6 +34,7 @@
 #include <type_traits>
 
 #include "archive_device.hh"
+#include "book_device.hh"
 #include "common.hh"
 #include "hf_device.hh"
 #include "kernels.hh"
@@ -2133,59 +2134,114 @@ k_chunk_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const 
 
 
 // =========================================================================================
-// sampled-codebook mode: one pass predicts and packs (psz_amd_set_codebook(SAMPLED))
+// sampled-codebook mode: sample -> device codebook -> one streaming pass
 // =========================================================================================
-// The codebook is built from the histogram of every kSampleStride-th brick, +1 on every bin so
-// every code is encodable, BEFORE the field is predicted.  One pass then predicts a brick, keeps
-// its codes in LDS (byte rows; a row with a code outside the byte window goes to global memory as
-// u16), learns its exact size in cells, takes its archive offset by a decoupled look-back over
-// the bricks before it and packs the rows straight into the archive: the codes never travel
-// through HBM and no plan pass runs.  Bricks are claimed in order from a ticket, so every brick a
-// look-back waits on is held by a running wave (the smallest unfinished brick never waits).
-// Codes, outliers and the reconstruction are the exact mode's; the codebook, hence the
-// bitstream, differs (chunks back to back, no gaps).
+// North-star pins the quant codes, the outliers and the reconstruction, not the bitstream, so
+// the codebook may come from a sample and the field need be read only once:
+//  * k_brick3_sample: the exact codes of a systematic 1/16 sample of 32 x 8 x 8 units (four 8^3
+//    tiles: the units cycle through every x position and visit every (y, z) tile row), one unit
+//    per wave step with all 8 z-rows in flight; its last workgroup builds the canonical codebook
+//    from sample + 1 per bin (every code encodable) on the device (book_device.hh) and writes the
+//    book and the archive's reverse book.  No host round trip.
+//  * k_brick3_stream: persistent waves claim bricks in order from a ticket; a wave predicts its
+//    brick row by row (rows streamed kStreamAhead ahead, across bricks), looks each row's four
+//    codewords per lane up in the LDS book and packs the row at once into its LDS staging buffer
+//    (the packing overlaps the loads in flight), publishes the brick's size, takes its archive
+//    offset by a decoupled look-back over the bricks before it (256 status words per step) and
+//    copies the packed brick out.  A brick that outgrows the staging takes its offset early and
+//    flushes as it goes.  Codes never travel through HBM; no plan pass; no gaps between bricks.
+//  * k_brick3_stream_finish: outlier segment (brick slots in brick order, then the spill list),
+//    totals, both headers; the last workgroup publishes the compress summary.
+// Deadlock-free: a look-back only waits on bricks claimed earlier, whose waves are running.
 constexpr uint32_t kSampleStride = 16;
 constexpr unsigned long long kStAgg = 1ull << 62, kStInc = 2ull << 62;  // look-back status flags
 
-// pass 0: the histogram of bricks 0, stride, 2 stride, ... (prediction as pass 1)
+// sample units of 32 x 8 x 8 elements; stride 16 from 4096 units up (>= 256 samples), else all
+__host__ __device__ inline uint32_t sample_units(uint32_t lx, uint32_t ly, uint32_t lz)
+{
+  return (lx / 32u) * ((ly + 7u) / 8u) * ((lz + 7u) / 8u);
+}
+__host__ __device__ inline uint32_t sample_stride(uint32_t units) { return units >= 256u * kSampleStride ? kSampleStride : 1u; }
+
+template <typename T>
+__device__ __forceinline__ T shfl_up8(T v)
+{
+  if constexpr (sizeof(T) == 4)
+    return __builtin_bit_cast(T, __shfl_up(__builtin_bit_cast(int, v), 8));
+  else {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const int lo = __shfl_up((int)(uint32_t)u, 8), hi = __shfl_up((int)(uint32_t)(u >> 32), 8);
+    return __builtin_bit_cast(T, (unsigned long long)(uint32_t)lo | ((unsigned long long)(uint32_t)hi << 32));
+  }
+}
+
+constexpr int kSampleThreads = hbook::kThreads;  // the last workgroup builds the book
 template <typename T, bool ZZ>
-__global__ void __launch_bounds__(64 * kBrickWaves)
+__global__ void __launch_bounds__(kSampleThreads)
 k_brick3_sample(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T ebx2_r, T r,
-                uint32_t* __restrict__ g_hist, int bklen, uint32_t nbx, uint32_t nby, uint32_t nbricks,
-                uint32_t stride)
+                uint32_t* __restrict__ g_hist, int bklen, uint32_t* ticket, uint32_t* book, uint8_t* revbook)
 {
   __shared__ uint32_t s_h[kMaxBklen];
+  __shared__ hbook::Smem s_book;
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   for (int i = threadIdx.x; i < bklen; i += blockDim.x) s_h[i] = 0;
   __syncthreads();
-  const StepLoader<T, 4> ld{in, (size_t)lx * ly, lx, ly, lz, nbx, nby, nbricks, 0, (uint32_t)lane};
-  const uint32_t nsamp = (nbricks + stride - 1) / stride;
-  for (uint32_t sidx = blockIdx.x * kBrickWaves + wid; sidx < nsamp; sidx += gridDim.x * kBrickWaves) {
-    const uint32_t brick = sidx * stride;
-    const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
-    const uint32_t x0 = bx * 256 + (uint32_t)lane * 4;
-    T bprev[8][4], raw[8][4], p[8][4];
-    ld.issue(brick, 0, raw);
-    for (int y = 0; y < 8; y++) {
-      prequant_ystep<T, 4>(raw, ebx2_r, p);
-      if (y + 1 < 8) ld.issue(brick, y + 1, raw);
-      residual_ystep<T, 4>(x0, y, bprev, p);
-      if (by * 8 + (uint32_t)y >= ly) break;
+  const uint32_t nux = lx / 32u, nuy = (ly + 7u) / 8u, units = sample_units(lx, ly, lz);
+  const uint32_t stride = sample_stride(units), nsamp = (units + stride - 1) / stride;
+  const size_t plane = (size_t)lx * ly;
+  const uint32_t ly_l = (uint32_t)lane >> 3, xq = (uint32_t)lane & 7u;
+  constexpr int kW = kSampleThreads / 64;
+  for (uint32_t i = blockIdx.x * kW + wid; i < nsamp; i += gridDim.x * kW) {
+    const uint32_t u = i * stride + i % stride;
+    if (u >= units) continue;  // (uniform)
+    const uint32_t ux = u % nux, t = u / nux, uy = t % nuy, uz = t / nuy;
+    const uint32_t y = uy * 8u + ly_l, x0 = ux * 32u + xq * 4u, z0 = uz * 8u;
+    T v[8][4];
 #pragma unroll
-      for (int z = 0; z < 8; z++) {
-        if (bz * 8 + (uint32_t)z >= lz) break;
+    for (int z = 0; z < 8; z++) {
+      const bool ok = y < ly && z0 + (uint32_t)z < lz;
+      load_row<T, 4>(in, (size_t)(z0 + z) * plane + (size_t)y * lx, x0, lx, ok, v[z]);
+    }
+    // prequant, z-diff, x-diff inside the 8-wide tile (two lanes), y-diff across lanes (the
+    // reference's order, lrz_c.cuhip.inl:341-352)
+    T a[8][4], pp[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-          bool ol;
-          float ov;
-          atomicAdd(&s_h[quantize<T, ZZ>(p[z][k], r, ol, ov)], 1u);
-        }
+    for (int z = 0; z < 8; z++)
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const T p = dround(v[z][k] * ebx2_r);
+        a[z][k] = z > 0 ? p - pp[k] : p;
+        pp[k] = p;
+      }
+#pragma unroll
+    for (int z = 0; z < 8; z++) {
+      const T west = shr_in_tile<T, 1, 2>(a[z][3]);
+#pragma unroll
+      for (int k = 3; k > 0; k--) a[z][k] = a[z][k] - a[z][k - 1];
+      if (lane & 1) a[z][0] = a[z][0] - west;
+    }
+#pragma unroll
+    for (int z = 0; z < 8; z++) {
+      const bool ok = y < ly && z0 + (uint32_t)z < lz;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const T north = shfl_up8(a[z][k]);
+        const T d = lane >= 8 ? a[z][k] - north : a[z][k];
+        bool ol;
+        float ov;
+        const uint16_t c = quantize<T, ZZ>(d, r, ol, ov);
+        if (ok) atomicAdd(&s_h[c], 1u);
       }
     }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < bklen; i += blockDim.x)
     if (s_h[i]) atomicAdd(&g_hist[i], s_h[i]);
+  if (!last_block(ticket)) return;
+  for (int i = threadIdx.x; i < bklen; i += blockDim.x)
+    s_h[i] = __hip_atomic_load(g_hist + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  hbook::build(s_h, bklen, 1u, book, revbook, s_book);
 }
 
 __device__ __forceinline__ unsigned long long st_word(unsigned long long flag, uint32_t cells, uint32_t oc)
@@ -2193,27 +2249,40 @@ __device__ __forceinline__ unsigned long long st_word(unsigned long long flag, u
   return flag | (unsigned long long)cells | ((unsigned long long)oc << 32);
 }
 
-// Exclusive prefix (cells, slot outliers) of `brick` from its predecessors' status words: 64 at
-// a time, back to the nearest one holding an inclusive prefix (lane 0 = brick - 1).  Bounded
-// spins: a word still empty after them counts as 0 and raises *timeout (never expected).
+// Exclusive prefix (cells, slot outliers) of `brick` from its predecessors' status words: 256 per
+// step (4 per lane, distance 4 lane + q), back to the nearest one holding an inclusive prefix.
+// Bounded spins: a word still empty after them counts as 0 and raises *timeout (never expected).
 __device__ __forceinline__ void lookback(const unsigned long long* status, uint32_t brick, int lane, uint32_t& xc,
                                          uint32_t& xo, unsigned int* timeout)
 {
   uint32_t sc = 0, so = 0;
-  for (int64_t j = (int64_t)brick - 1;; j -= 64) {
-    const int64_t me = j - lane;
-    unsigned long long v = kStInc;  // before brick 0: an inclusive prefix of 0
-    if (me >= 0) {
-      uint32_t spins = 0;
-      do
-        v = __hip_atomic_load(status + me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      while ((v >> 62) == 0 && ++spins < (1u << 22));
-      if ((v >> 62) == 0) atomicOr(timeout, 1u);
+  for (int64_t j = (int64_t)brick - 1;; j -= 256) {
+    unsigned long long v[4];
+    uint32_t qinc = 4;  // this lane's nearest inclusive word (4: none)
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int64_t me = j - 4 * lane - q;
+      v[q] = kStInc;  // before brick 0: an inclusive prefix of 0
+      if (me >= 0) {
+        uint32_t spins = 0;
+        do
+          v[q] = __hip_atomic_load(status + me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while ((v[q] >> 62) == 0 && ++spins < (1u << 22));
+        if ((v[q] >> 62) == 0) atomicOr(timeout, 1u);
+      }
     }
-    const uint64_t inc = __builtin_amdgcn_ballot_w64((v >> 62) == 2);
-    const int k = inc ? __builtin_ctzll(inc) : 64;
-    const bool take = lane <= k;
-    const uint32_t c = take ? (uint32_t)v : 0u, o = take ? (uint32_t)(v >> 32) & 0x3FFFFFFFu : 0u;
+#pragma unroll
+    for (int q = 3; q >= 0; q--)
+      if ((v[q] >> 62) == 2) qinc = (uint32_t)q;
+    const uint64_t inc = __builtin_amdgcn_ballot_w64(qinc < 4);
+    const int k = inc ? __builtin_ctzll(inc) : 64;  // the lane holding the nearest inclusive word
+    uint32_t c = 0, o = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const bool take = lane < k || (lane == k && (uint32_t)q <= qinc);
+      c += take ? (uint32_t)v[q] : 0u;
+      o += take ? (uint32_t)(v[q] >> 32) & 0x3FFFFFFFu : 0u;
+    }
     sc += readlane(hfd::wave_incl_scan(c), 63);
     so += readlane(hfd::wave_incl_scan(o), 63);
     if (inc) break;
@@ -2221,15 +2290,15 @@ __device__ __forceinline__ void lookback(const unsigned long long* status, uint3
   xc = sc, xo = so;
 }
 
-struct SingleArgs {
+struct StreamArgs {
   uint32_t lx, ly, lz, nbx, nby, nbricks;
   OutlierSink ol;
-  BrickCodes bcs;  // c16: the u16 rows (brick order); c0
   const uint32_t* book;
   int bklen;
   uint32_t* par_nbit;
   uint32_t* par_entry;
   uint32_t* bitstream;
+  uint32_t bs_cap;             // bitstream capacity (cells)
   unsigned long long* status;  // per brick, zeroed per call
   uint32_t* ticket;            // zeroed per call
   uint32_t* ol_pre;            // per brick: exclusive prefix of slot outliers
@@ -2237,34 +2306,32 @@ struct SingleArgs {
   unsigned int* timeout;
 };
 
-constexpr int kSingleWaveWords = 64 * 64 + pack_cells_words<4>();  // byte rows + packing cells
-#ifndef CUSZ_AMD_SINGLE_AHEAD
-#define CUSZ_AMD_SINGLE_AHEAD 16
-#endif
+constexpr int kStreamWaves = 4;
+constexpr int kStageWords = 4608;  // per-wave staging of the packed brick (18 KB: 8 waves per CU)
+static_assert(kStageWords >= 2 * kPackRowMax, "a brick row always fits");
+template <typename T>
+constexpr int kStreamAhead = 8;  // rows in flight per wave
 
 template <typename T, bool ZZ>
-__global__ void __launch_bounds__(64 * kBrickWaves)
-k_brick3_single(const T* __restrict__ in, SingleArgs a, T ebx2_r, T r)
+__global__ void __launch_bounds__(64 * kStreamWaves) __attribute__((amdgpu_waves_per_eu(1, 2)))  // LDS: 2 per SIMD
+k_brick3_stream(const T* __restrict__ in, StreamArgs a, T ebx2_r, T r)
 {
   constexpr int V = 4;
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t* s_book = smem;
+  __shared__ uint32_t s_book[kMaxBklen];
+  __shared__ uint32_t s_stage[kStreamWaves][kStageWords + 4];  // + pack4_or_lj's zero slack
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint32_t* rows8 = smem + kMaxBklen + wid * kSingleWaveWords;  // 64 byte rows of 256
-  uint32_t* cells = rows8 + 64 * 64;
+  uint32_t* const stage = s_stage[wid];
   for (int i = threadIdx.x; i < a.bklen; i += blockDim.x) s_book[i] = a.book[i];
-  for (int i = lane; i < pack_cells_words<V>(); i += 64) cells[i] = 0;
+  for (int i = lane; i < kStageWords + 4; i += 64) stage[i] = 0;
   __syncthreads();
   const StepLoader<T, V> ld{in, (size_t)a.lx * a.ly, a.lx, a.ly, a.lz, a.nbx, a.nby, a.nbricks, 0, (uint32_t)lane};
   const size_t plane = ld.plane;
-  const uint32_t c0 = a.bcs.c0;
   auto claim = [&]() -> uint32_t {
     uint32_t b = 0;
     if (lane == 0) b = atomicAdd(a.ticket, 1u);
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
   };
-  // rows in flight per wave: two y-steps (f32), as LDS allows only 8 waves per CU here
-  constexpr int D = sizeof(T) == 4 ? CUSZ_AMD_SINGLE_AHEAD : 8;
+  constexpr int D = kStreamAhead<T>;
   uint32_t brick = claim();
   T q[D][V];
 #pragma unroll
@@ -2274,16 +2341,31 @@ k_brick3_single(const T* __restrict__ in, SingleArgs a, T ebx2_r, T r)
     const uint32_t bx = brick % a.nbx, t = brick / a.nbx, by = t % a.nby, bz = t / a.nby;
     const uint32_t x0 = bx * (64 * V) + lane * V, y0 = by * 8, z0 = bz * 8;
     const uint32_t nyv = min(8u, a.ly - y0), nzv = min(8u, a.lz - z0);
-    uint16_t* cbrick = a.bcs.c16 + (size_t)brick * 64 * (64 * V) + (size_t)lane * V;
-    uint64_t rowmask = 0;
-    uint32_t cnt = 0, bcells = 0;
+    uint32_t cnt = 0;               // outliers of the brick
+    uint32_t off = 0, fbase = 0;    // brick words packed; words [fbase, off) are in the staging
+    uint32_t xc = 0, xo = 0;        // the brick's archive offsets (known early when it flushes)
+    bool direct = false;            // (uniform) offsets taken early: flushes go straight out
     unsigned long long bbits = 0;
+    uint32_t my_nbit = 0, my_loc = 0;  // lane = row: its bits and first word in the brick
+    // staged words -> the archive (each lane one word per store: the offset has any alignment)
+    auto flush = [&]() {
+      hfd::wave_sync();
+      const uint32_t m = off - fbase;
+      const bool fits = xc + off <= a.bs_cap;
+      if (!fits && lane == 0) atomicOr(a.timeout, 4u);
+      for (uint32_t i = (uint32_t)lane; i < m; i += 64) {
+        const uint32_t v = stage[i];
+        stage[i] = 0;
+        if (fits) a.bitstream[xc + fbase + i] = v;
+      }
+      fbase = off;
+      hfd::wave_sync();
+    };
     T bprev[8][V], pprev[V];
 #pragma unroll
     for (int z = 0; z < 8; z++)
 #pragma unroll
       for (int k = 0; k < V; k++) bprev[z][k] = (T)0;
-    // phase 1: predict, codes into LDS (or u16 rows to global), outliers into the brick's slot
 #pragma unroll 1
     for (int r0 = 0; r0 < 64; r0 += D)
 #pragma unroll
@@ -2315,28 +2397,14 @@ k_brick3_single(const T* __restrict__ in, SingleArgs a, T ebx2_r, T r)
         float olv[V];
         uint16_t qc[V];
         uint64_t anyol = 0;
-        uint32_t bits = 0;
-        bool wide = false;
+        uint32_t w[V], bits = 0;
 #pragma unroll
         for (int k = 0; k < V; k++) {
           bool is_ol;
           qc[k] = quantize<T, ZZ>(d[k], r, is_ol, olv[k]);
           anyol |= __ballot(is_ol);
-          bits += s_book[qc[k]] >> 27;
-          wide |= (uint32_t)qc[k] - c0 > 254u && qc[k] != 0;
-        }
-        const uint32_t rb = readlane(hfd::wave_incl_scan(bits), 63);
-        bbits += rb;
-        bcells += (rb + 31u) >> 5;
-        if (__builtin_amdgcn_ballot_w64(wide)) {
-          store_codes_row<V>(cbrick + (size_t)row * (64 * V), qc);
-          rowmask |= 1ull << row;
-        }
-        else {
-          uint32_t w = 0;
-#pragma unroll
-          for (int k = 0; k < V; k++) w |= (qc[k] == 0 ? 255u : (uint32_t)qc[k] - c0) << (8 * k);
-          rows8[row * 64 + lane] = w;
+          w[k] = s_book[qc[k]];
+          bits += w[k] >> 27;
         }
         if (anyol) {
           uint32_t mask = 0;
@@ -2349,18 +2417,43 @@ k_brick3_single(const T* __restrict__ in, SingleArgs a, T ebx2_r, T r)
           }
           emit_outliers<V>(a.ol, brick, cnt, mask, olv, idx);
         }
+        const uint32_t inc = hfd::wave_incl_scan(bits);
+        const uint32_t tot = readlane(inc, 63);
+        if (off - fbase + kPackRowMax > kStageWords) {  // the staging is full: offsets now, flush
+          if (!direct) {
+            lookback(a.status, brick, lane, xc, xo, a.timeout);
+            direct = true;
+          }
+          flush();
+        }
+        const uint32_t pos = ((off - fbase) << 5) + inc - bits;
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(bits > 64u) == 0, 1))
+          hfd::pack4_or_lj(stage, pos, w, bits);
+        else
+          hfd::pack_words<V>(stage, pos, w, V);
+        if ((uint32_t)lane == (uint32_t)row) my_nbit = tot, my_loc = off;
+        off += (tot + 31) >> 5;
+        bbits += tot;
       }
     // the brick's place in the archive
     const uint32_t oc = min(cnt, a.ol.cap_per_brick);
-    uint32_t xc = 0, xo = 0;
-    if (brick == 0) {
-      if (lane == 0) __hip_atomic_store(a.status, st_word(kStInc, bcells, oc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!direct) {
+      if (brick == 0) {
+        if (lane == 0) __hip_atomic_store(a.status, st_word(kStInc, off, oc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      else {
+        if (lane == 0) __hip_atomic_store(a.status + brick, st_word(kStAgg, off, oc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lookback(a.status, brick, lane, xc, xo, a.timeout);
+      }
     }
-    else {
-      if (lane == 0) __hip_atomic_store(a.status + brick, st_word(kStAgg, bcells, oc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      lookback(a.status, brick, lane, xc, xo, a.timeout);
-      if (lane == 0)
-        __hip_atomic_store(a.status + brick, st_word(kStInc, xc + bcells, xo + oc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0 && (direct || brick != 0))
+      __hip_atomic_store(a.status + brick, st_word(kStInc, xc + off, xo + oc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flush();
+    const uint32_t ry = lane >> 3, rz = lane & 7;
+    if (ry < nyv && rz < nzv) {
+      const size_t c = ((size_t)(z0 + rz) * a.ly + (y0 + ry)) * a.nbx + bx;
+      a.par_nbit[c] = my_nbit;
+      a.par_entry[c] = xc + my_loc;
     }
     if (lane == 0) {
       a.ol.brick_cnt[brick] = cnt;
@@ -2368,64 +2461,13 @@ k_brick3_single(const T* __restrict__ in, SingleArgs a, T ebx2_r, T r)
       a.ol_pre[brick] = xo;
       atomicAdd(&a.info->total_nbit, bbits);
     }
-    hfd::wave_sync();
-    // phase 2: pack the rows (k_brick3_pack's row loop) at cell xc onwards, back to back; the
-    // u16 rows this wave stored are read back (their stores drained first)
-    if (rowmask) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint32_t* dst = a.bitstream + xc;
-    uint32_t off = 0, my_nbit = 0, my_entry = 0;
-    for (uint32_t y = 0; y < nyv; y++)
-      for (uint32_t z = 0; z < nzv; z++) {
-        const uint32_t row = y * 8 + z;
-        uint32_t qs[4];
-        if ((rowmask >> row) & 1ull) {
-          uint2 v;
-          __builtin_memcpy(&v, cbrick + (size_t)row * (64 * V), 8);
-          qs[0] = v.x & 0xFFFFu, qs[1] = v.x >> 16, qs[2] = v.y & 0xFFFFu, qs[3] = v.y >> 16;
-        }
-        else {
-          const uint32_t w8 = rows8[row * 64 + lane];
-#pragma unroll
-          for (int k = 0; k < 4; k++) {
-            const uint32_t b = (w8 >> (8 * k)) & 255u;
-            qs[k] = b == 255u ? 0u : b + c0;
-          }
-        }
-        uint32_t w[V], bits = 0;
-#pragma unroll
-        for (int k = 0; k < V; k++) {
-          w[k] = s_book[qs[k]];
-          bits += w[k] >> 27;
-        }
-        const uint32_t inc = hfd::wave_incl_scan(bits);
-        const uint32_t tot = readlane(inc, 63);
-        if (__builtin_expect(__builtin_amdgcn_ballot_w64(bits > 64u) == 0, 1))
-          hfd::pack4_or(cells, inc - bits, w, bits);
-        else
-          hfd::pack_words<V>(cells, inc - bits, w, V);
-        hfd::wave_sync();
-        const uint32_t nc = (tot + 31) >> 5;
-        for (uint32_t i = lane; i < nc; i += 64) {
-          dst[off + i] = cells[i];
-          cells[i] = 0;
-        }
-        if ((uint32_t)lane == row) my_nbit = tot, my_entry = xc + off;
-        off += nc;
-        hfd::wave_sync();
-      }
-    const uint32_t ry = lane >> 3, rz = lane & 7;
-    if (ry < nyv && rz < nzv) {
-      const size_t c = ((size_t)(z0 + rz) * a.ly + (y0 + ry)) * a.nbx + bx;
-      a.par_nbit[c] = my_nbit;
-      a.par_entry[c] = my_entry;
-    }
     brick = bnext;
   }
 }
 
-// after the single pass: the outlier segment (slots in brick order, then the spill list), the
+// after the streaming pass: the outlier segment (slots in brick order, then the spill list), the
 // totals and both headers; the last workgroup publishes the compress summary
-__global__ void __launch_bounds__(256) k_brick3_single_finish(SingleArgs a, HeaderTpl tpl, uint8_t* archive,
+__global__ void __launch_bounds__(256) k_brick3_stream_finish(StreamArgs a, HeaderTpl tpl, uint8_t* archive,
                                                               size_t phf_offset, size_t bits_rel, HostPub pub)
 {
   const unsigned long long last =
@@ -2586,61 +2628,64 @@ int launch_brick_pack(const BrickLaunch& L, const BrickCodes& bcodes, const uint
 
 template <typename T>
 int launch_brick_sample(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, uint32_t* hist, int bklen,
-                        hipStream_t st)
+                        uint32_t* ticket, uint32_t* book, uint8_t* revbook, hipStream_t st)
 {
   const BrickGeom& g = L.g;
-  if (g.ndim != 3) return (int)hipErrorInvalidValue;
+  if (g.ndim != 3 || bklen > hbook::kThreads) return (int)hipErrorInvalidValue;
   const T ebx2_r = (T)(1.0 / (eb * 2)), r = (T)radius;
-  const uint32_t stride = g.nbricks >= 64 * kSampleStride ? kSampleStride : 1u;
-  const uint32_t nsamp = (g.nbricks + stride - 1) / stride;
-  const uint32_t grid = std::max(1u, std::min((nsamp + kBrickWaves - 1) / kBrickWaves, (uint32_t)L.ncu * 4));
+  const uint32_t units = sample_units(L.lx, L.ly, L.lz), stride = sample_stride(units);
+  const uint32_t nsamp = (units + stride - 1) / stride;
+  constexpr uint32_t kW = kSampleThreads / 64;
+  const uint32_t grid = std::max(1u, std::min((nsamp + kW - 1) / kW, (uint32_t)L.ncu));
   if (zz)
-    k_brick3_sample<T, true><<<grid, 64 * kBrickWaves, 0, st>>>(in, L.lx, L.ly, L.lz, ebx2_r, r, hist, bklen, g.nbx,
-                                                                g.nby, g.nbricks, stride);
+    k_brick3_sample<T, true><<<grid, kSampleThreads, 0, st>>>(in, L.lx, L.ly, L.lz, ebx2_r, r, hist, bklen, ticket,
+                                                               book, revbook);
   else
-    k_brick3_sample<T, false><<<grid, 64 * kBrickWaves, 0, st>>>(in, L.lx, L.ly, L.lz, ebx2_r, r, hist, bklen, g.nbx,
-                                                                 g.nby, g.nbricks, stride);
+    k_brick3_sample<T, false><<<grid, kSampleThreads, 0, st>>>(in, L.lx, L.ly, L.lz, ebx2_r, r, hist, bklen, ticket,
+                                                                book, revbook);
   return (int)hipGetLastError();
 }
 
 template <typename T>
-int launch_brick_single(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const BrickSingle& s,
+int launch_brick_stream(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const BrickSingle& s,
                         const void* psz_tpl, const void* phf_tpl, hipStream_t st, const HostPub& pub)
 {
   const BrickGeom& g = L.g;
   if (g.ndim != 3) return (int)hipErrorInvalidValue;
   const T ebx2_r = (T)(1.0 / (eb * 2)), r = (T)radius;
-  SingleArgs a{L.lx, L.ly, L.lz, g.nbx, g.nby, g.nbricks, s.ol, s.bcs, s.book, s.bklen, s.par_nbit, s.par_entry,
-               s.bitstream, s.status, s.ticket, s.ol_pre, s.info, s.timeout};
-  const size_t lds = ((size_t)kMaxBklen + (size_t)kBrickWaves * kSingleWaveWords) * 4;
+  StreamArgs a{L.lx, L.ly, L.lz, g.nbx, g.nby, g.nbricks, s.ol, s.book, s.bklen, s.par_nbit, s.par_entry,
+               s.bitstream, s.bs_cap, s.status, s.ticket, s.ol_pre, s.info, s.timeout};
   static int per_cu[2] = {0, 0};
   int& pc = per_cu[sizeof(T) == 8];
   if (!pc) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k_brick3_single<T, false>, 64 * kBrickWaves, lds) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k_brick3_stream<T, false>, 64 * kStreamWaves, 0) != hipSuccess ||
         pc < 1)
       pc = 1;
   }
   // persistent waves claim bricks from the ticket; every one must be resident (the look-back
   // waits only on claimed bricks, and a claimed brick's wave is running)
-  const uint32_t grid = std::max(1u, std::min((g.nbricks + kBrickWaves - 1) / kBrickWaves, (uint32_t)(pc * L.ncu)));
+  const uint32_t grid =
+      std::max(1u, std::min((g.nbricks + kStreamWaves - 1) / kStreamWaves, (uint32_t)(pc * L.ncu)));
   if (zz)
-    k_brick3_single<T, true><<<grid, 64 * kBrickWaves, lds, st>>>(in, a, ebx2_r, r);
+    k_brick3_stream<T, true><<<grid, 64 * kStreamWaves, 0, st>>>(in, a, ebx2_r, r);
   else
-    k_brick3_single<T, false><<<grid, 64 * kBrickWaves, lds, st>>>(in, a, ebx2_r, r);
+    k_brick3_stream<T, false><<<grid, 64 * kStreamWaves, 0, st>>>(in, a, ebx2_r, r);
   if (hipError_t e = hipGetLastError()) return (int)e;
   HeaderTpl t;
   __builtin_memcpy(t.psz, psz_tpl, 176);
   __builtin_memcpy(t.phf, phf_tpl, 64);
   const uint32_t fgrid = std::max(1u, std::min((g.nbricks + 3) / 4, 1024u));
-  k_brick3_single_finish<<<fgrid, 256, 0, st>>>(a, t, s.archive, s.phf_offset, s.bits_rel, pub);
+  k_brick3_stream_finish<<<fgrid, 256, 0, st>>>(a, t, s.archive, s.phf_offset, s.bits_rel, pub);
   return (int)hipGetLastError();
 }
 
-template int launch_brick_sample<float>(const BrickLaunch&, const float*, double, int, bool, uint32_t*, int, hipStream_t);
-template int launch_brick_sample<double>(const BrickLaunch&, const double*, double, int, bool, uint32_t*, int, hipStream_t);
-template int launch_brick_single<float>(const BrickLaunch&, const float*, double, int, bool, const BrickSingle&,
+template int launch_brick_sample<float>(const BrickLaunch&, const float*, double, int, bool, uint32_t*, int,
+                                        uint32_t*, uint32_t*, uint8_t*, hipStream_t);
+template int launch_brick_sample<double>(const BrickLaunch&, const double*, double, int, bool, uint32_t*, int,
+                                         uint32_t*, uint32_t*, uint8_t*, hipStream_t);
+template int launch_brick_stream<float>(const BrickLaunch&, const float*, double, int, bool, const BrickSingle&,
                                         const void*, const void*, hipStream_t, const HostPub&);
-template int launch_brick_single<double>(const BrickLaunch&, const double*, double, int, bool, const BrickSingle&,
+template int launch_brick_stream<double>(const BrickLaunch&, const double*, double, int, bool, const BrickSingle&,
                                          const void*, const void*, hipStream_t, const HostPub&);
 
 int launch_brick_cell_bounds(const BrickLaunch& L, const uint32_t* cells, size_t ncell, uint32_t* bstart,

@@ -148,6 +148,9 @@ int launch_upload(const XferRegions& r, hipStream_t st);
 int launch_gate_upload(const XferRegions& r, const uint32_t* gate, uint32_t epoch, unsigned int* timeout,
                        hipStream_t st);
 int launch_zero(const XferRegions& r, hipStream_t st);  // dst/nwords only
+// device codebook (book_device.hh): one workgroup, histogram (+ smooth per bin) -> book + revbook
+int launch_book_device(const uint32_t* hist, int bklen, uint32_t smooth, uint32_t* book, uint8_t* revbook,
+                       hipStream_t st);
 int launch_excess(const uint32_t* spill_cnt, uint32_t cap, uint32_t* dst, hipStream_t st);
 
 // ---- cuSZ-i spline3 (spline.hip) -----------------------------------------------------------
@@ -273,18 +276,12 @@ int launch_brick_plan(const BrickLaunch& L, const BrickPlanArgs& a, const void* 
 int launch_brick_pack(const BrickLaunch& L, const BrickCodes& bc, const uint32_t* book, int bklen,
                       const BrickPlanArgs& plan, uint32_t* par_nbit, uint32_t* par_entry, uint32_t* bitstream,
                       int reverse, unsigned int* overflow, hipStream_t st, const HostPub& pub = HostPub{});
-// sampled-codebook mode (3-D bricks): pass 0 = the histogram of every 16th brick; then one pass
-// predicts, sizes (decoupled look-back over the bricks) and packs each brick into the archive,
-// and a finish kernel writes the outlier segment, the totals and the headers
-template <typename T>
-int launch_brick_sample(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, uint32_t* hist, int bklen,
-                        hipStream_t st);
 struct BrickSingle {
   OutlierSink ol;
-  BrickCodes bcs;  // c16: u16 rows; c0
   const uint32_t* book;
   int bklen;
   uint32_t *par_nbit, *par_entry, *bitstream;
+  uint32_t bs_cap;             // bitstream capacity (cells)
   unsigned long long* status;  // nbricks words, zeroed per call
   uint32_t* ticket;            // zeroed per call
   uint32_t* ol_pre;            // nbricks
@@ -293,8 +290,14 @@ struct BrickSingle {
   uint8_t* archive;
   size_t phf_offset, bits_rel;
 };
+// sampled-codebook mode (brick.hip): the sample histogram and, in the sample kernel's last
+// workgroup, the device codebook (book + the archive's reverse book); then the streaming pass
+// (+ finish: outlier segment, headers, the compress summary)
 template <typename T>
-int launch_brick_single(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const BrickSingle& s,
+int launch_brick_sample(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, uint32_t* hist, int bklen,
+                        uint32_t* ticket, uint32_t* book, uint8_t* revbook, hipStream_t st);
+template <typename T>
+int launch_brick_stream(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const BrickSingle& s,
                         const void* psz_tpl, const void* phf_tpl, hipStream_t st, const HostPub& pub);
 // Outlier cells for the fused decoder: when the archive's cells are grouped by brick and sorted
 // by (row, x) (k_brick_cell_bounds checks; this compressor writes them so), the decoder ranks the

@@ -784,19 +784,16 @@ struct Pipeline {
                                                stream));
     mark(1);
     last_layout = PSZ_AMD_LAYOUT_BRICK;
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_sample<T>(bl, in, eb, radius, zz, d_hist, bklen, stream));
-    mark(2);
-    int fs = fetch(regions({{h_hist(), d_hist, (size_t)bklen * 4}}), 2);
-    if (fs) return fs;
-    for (int i = 0; i < bklen; i++) h_hist()[i] += 1;  // every code encodable
-    build_codebook(h_hist(), bklen, h_book(), h_revbook());
     const size_t phf_off = 176;
     const size_t rvbk = rvbk_bytes(bklen);
     const int bsub = g.W, bpar = (int)g.nchunks;
     const size_t nbit_rel = 128 + rvbk, entry_rel = nbit_rel + 4 * (size_t)bpar;
     const size_t bits_rel = entry_rel + 4 * (size_t)bpar;
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_upload(
-        regions({{d_book, h_book(), (size_t)bklen * 4}, {d_archive + phf_off + 128, h_revbook(), rvbk}}), stream));
+    // sample histogram; its last workgroup builds the codebook on the device (book_device.hh):
+    // the book, and the reverse book straight into the archive
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_sample<T>(bl, in, eb, radius, zz, d_hist, bklen, hist_ticket(), d_book,
+                                                          d_archive + phf_off + 128, stream));
+    mark(2);
     mark(3);
     h->vle_sublen = bsub;
     h->vle_pardeg = bpar;
@@ -807,13 +804,14 @@ struct Pipeline {
     ph.bklen = bklen, ph.sublen = bsub, ph.pardeg = bpar, ph.original_len = n;
     ph.entry[0] = 0, ph.entry[1] = 128, ph.entry[2] = (uint32_t)nbit_rel, ph.entry[3] = (uint32_t)entry_rel;
     ph.entry[4] = (uint32_t)bits_rel;
+    const size_t chunks = std::max((size_t)pardeg, (size_t)g.nchunks);
     BrickSingle sg{OutlierSink{d_slots, d_brick_cnt, d_spill, spill_cnt(), brick_cap(), spill_cap, nullptr},
-                   brick_codes(zz, radius),
                    d_book,
                    bklen,
                    reinterpret_cast<uint32_t*>(d_archive + phf_off + nbit_rel),
                    reinterpret_cast<uint32_t*>(d_archive + phf_off + entry_rel),
                    reinterpret_cast<uint32_t*>(d_archive + phf_off + bits_rel),
+                   (uint32_t)std::min<size_t>(bitstream_cells_cap() + chunks, 0xFFFFFFFFu),
                    status,
                    &info()->ticket,
                    d_ub,
@@ -823,7 +821,7 @@ struct Pipeline {
                    phf_off,
                    bits_rel};
     const HostPub sp{readback_regions(), const_cast<uint32_t*>(flag(3)), ++epoch, summary_ticket()};
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_single<T>(bl, in, eb, radius, zz, sg, h, &ph, stream, sp));
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_stream<T>(bl, in, eb, radius, zz, sg, h, &ph, stream, sp));
     summary_epoch = sp.epoch;
     mark(4);
     mark(5);
@@ -1388,6 +1386,15 @@ int psz_amd_decode_codes(psz_resource* m, uint8_t* in)
 const char* psz_amd_version(void) { return "cusz_amd 0.1 (gfx950)"; }
 
 int psz_amd_last_create_status(void) { return g_create_status; }
+
+int psz_amd_build_book_device(const uint32_t* IN_d_hist, int bklen, uint32_t smooth, uint32_t* OUT_d_book,
+                              uint8_t* OUT_d_revbook, void* stream)
+{
+  if (!IN_d_hist || !OUT_d_book || !OUT_d_revbook || bklen < 1 || bklen > 1024) return PSZ_AMD_ERR_INVALID_ARG;
+  CUSZ_AMD_HIP_CHECK((hipError_t)cusz_amd::launch_book_device(IN_d_hist, bklen, smooth, OUT_d_book, OUT_d_revbook,
+                                                                (hipStream_t)stream));
+  return PSZ_SUCCESS;
+}
 
 // internal: the older API passes a stream per call (cusz.h psz_compress/psz_decompress)
 int cusz_amd_set_stream(psz_resource* m, void* stream)

@@ -18,9 +18,11 @@ namespace cusz_amd {
 constexpr uint32_t kPubGroups = 8;
 constexpr uint32_t kPubTicketWords = kPubGroups + 1;
 
-__device__ __forceinline__ void publish_last(const HostPub& pub)
+// true in every thread of the workgroup that finishes last (ticket: kPubTicketWords words, zeroed
+// per call); every thread of every workgroup must call it.  The others' global writes and atomics
+// are then complete (read them back by agent-scope atomic loads).
+__device__ __forceinline__ bool last_block(uint32_t* ticket)
 {
-  if (!pub.flag) return;
   __shared__ uint32_t s_last;
   __builtin_amdgcn_s_waitcnt(0);  // this wave's stores and atomics have completed
   __syncthreads();
@@ -29,12 +31,18 @@ __device__ __forceinline__ void publish_last(const HostPub& pub)
     const uint32_t in_group = n / kPubGroups + (g < n % kPubGroups ? 1u : 0u);
     const uint32_t groups = n < kPubGroups ? n : kPubGroups;
     bool last = false;
-    if (__hip_atomic_fetch_add(pub.ticket + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_group - 1)
-      last = __hip_atomic_fetch_add(pub.ticket + kPubGroups, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == groups - 1;
+    if (__hip_atomic_fetch_add(ticket + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_group - 1)
+      last = __hip_atomic_fetch_add(ticket + kPubGroups, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == groups - 1;
     s_last = last;
   }
   __syncthreads();
-  if (!s_last) return;
+  return s_last != 0;
+}
+
+__device__ __forceinline__ void publish_last(const HostPub& pub)
+{
+  if (!pub.flag) return;
+  if (!last_block(pub.ticket)) return;
   for (int k = 0; k < pub.r.count; k++)
     for (int i = threadIdx.x; i < pub.r.nwords[k]; i += blockDim.x)
       pub.r.dst[k][i] = __hip_atomic_load(pub.r.src[k] + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -432,12 +432,97 @@ int orc_huffman_lengths(const uint32_t* hist, int bklen, uint8_t* lens)
 }
 
 /* canonisation, hf_canon.seq.cc:105-161; book word = code | len<<27 (hf_impl.hh:40-59) */
+static int canonize_lengths(uint8_t* lens, int bklen, uint32_t* book, uint8_t* revbook);
+
 int orc_build_codebook_u2(const uint32_t* hist, int bklen, uint32_t* book, uint8_t* revbook)
+{
+  uint8_t* lens = (uint8_t*)malloc(bklen);
+  orc_huffman_lengths(hist, bklen, lens);
+  return canonize_lengths(lens, bklen, book, revbook);
+}
+
+/* ------------------------------------------------------------------------- */
+/* Device codebook (cusz_amd/csrc/book_device.hh) restated serially: NOT the reference's heap.  */
+/* Optimal code lengths by the two-queue Huffman construction: leaves sorted by (weight, symbol), */
+/* internal nodes in creation order (their weights never decrease), at each merge the two       */
+/* smallest heads with a leaf taken before an internal node of equal weight.  Weights are       */
+/* hist + smooth (smooth = 1: every symbol encodable, the sampled-codebook mode); a tree deeper  */
+/* than 27 bits halves every weight ((w + 1) / 2, never 0) and is rebuilt.  Canonisation as the  */
+/* reference's (canonize_lengths).  Test infrastructure: the device book is checked against it. */
+/* ------------------------------------------------------------------------- */
+
+static int twoqueue_lengths(const uint64_t* w, int bklen, uint8_t* lens)
+{
+  int n = 0;
+  int* sym = (int*)malloc(sizeof(int) * bklen);
+  for (int s = 0; s < bklen; s++)
+    if (w[s]) sym[n++] = s;
+  memset(lens, 0, bklen);
+  if (n == 0) {
+    free(sym);
+    return 0;
+  }
+  if (n == 1) {
+    lens[sym[0]] = 1;
+    free(sym);
+    return 1;
+  }
+  /* stable sort of the used symbols by weight (insertion sort: ties keep symbol order) */
+  for (int i = 1; i < n; i++) {
+    int v = sym[i], j = i - 1;
+    while (j >= 0 && w[sym[j]] > w[v]) sym[j + 1] = sym[j], j--;
+    sym[j + 1] = v;
+  }
+  uint64_t* iw = (uint64_t*)malloc(sizeof(uint64_t) * n);
+  int* par = (int*)malloc(sizeof(int) * 2 * n);  /* leaves 0..n-1 (sorted order), internals n.. */
+  int li = 0, ii = 0, ni = 0;
+  while ((n - li) + (ni - ii) > 1) {
+    int pick[2];
+    uint64_t pw[2];
+    for (int k = 0; k < 2; k++) {
+      const int hasl = li < n, hasi = ii < ni;
+      if (hasl && (!hasi || w[sym[li]] <= iw[ii])) pick[k] = li, pw[k] = w[sym[li]], li++;
+      else pick[k] = n + ii, pw[k] = iw[ii], ii++;
+    }
+    par[pick[0]] = par[pick[1]] = n + ni;
+    iw[ni++] = pw[0] + pw[1];
+  }
+  /* depths: the root is the last internal node; parents come after their children */
+  int* depth = (int*)malloc(sizeof(int) * 2 * n);
+  const int root = n + ni - 1;
+  int maxl = 0;
+  depth[root] = 0;
+  for (int id = root - 1; id >= 0; id--) {
+    depth[id] = depth[par[id]] + 1;
+    if (id < n) {
+      lens[sym[id]] = (uint8_t)(depth[id] > 255 ? 255 : depth[id]);
+      if (depth[id] > maxl) maxl = depth[id];
+    }
+  }
+  free(depth);
+  free(par);
+  free(iw);
+  free(sym);
+  return maxl;
+}
+
+int orc_book_twoqueue_u2(const uint32_t* hist, int bklen, uint32_t smooth, uint32_t* book, uint8_t* revbook)
+{
+  uint64_t* w = (uint64_t*)malloc(sizeof(uint64_t) * bklen);
+  uint8_t* lens = (uint8_t*)malloc(bklen);
+  for (int s = 0; s < bklen; s++) w[s] = (uint64_t)hist[s] + smooth;
+  while (twoqueue_lengths(w, bklen, lens) > ORC_LMAX)
+    for (int s = 0; s < bklen; s++)
+      if (w[s]) w[s] = (w[s] + 1) / 2;
+  free(w);
+  return canonize_lengths(lens, bklen, book, revbook);
+}
+
+/* lens: consumed (freed) */
+static int canonize_lengths(uint8_t* lens, int bklen, uint32_t* book, uint8_t* revbook)
 {
   const int TB = 32;
   int rvbk_bytes = 4 * (2 * TB) + 2 * bklen;
-  uint8_t* lens = (uint8_t*)malloc(bklen);
-  orc_huffman_lengths(hist, bklen, lens);
 
   int numl[32] = {0}, iterby[32] = {0}, first[32] = {0}, entry[32] = {0};
   uint16_t* keys = (uint16_t*)calloc(bklen, sizeof(uint16_t));

@@ -56,6 +56,11 @@ int orc_build_codebook_u2(const uint32_t* hist, int bklen, uint32_t* book, uint8
 /* code lengths only (before canonisation); returns max length */
 int orc_huffman_lengths(const uint32_t* hist, int bklen, uint8_t* lens);
 
+/* The device codebook's algorithm (cusz_amd/csrc/book_device.hh), serially: two-queue Huffman
+ * over (weight, symbol)-sorted leaves of hist + smooth, leaf first on equal weights, depth > 27
+ * halves the weights and rebuilds; reference canonisation.  Returns revbook bytes. */
+int orc_book_twoqueue_u2(const uint32_t* hist, int bklen, uint32_t smooth, uint32_t* book, uint8_t* revbook);
+
 /* chunking (codec/hf/src/libphf.cc:26-70); n_cu = #CUs, max_threads = max threads/block */
 void orc_coarse_tune(size_t len, int n_cu, int max_threads, int* sublen, int* pardeg);
 

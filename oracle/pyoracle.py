@@ -61,6 +61,8 @@ def lib():
         L.orc_build_codebook_u2.argtypes = [_P, C.c_int, _P, _P]
         L.orc_huffman_lengths.restype = C.c_int
         L.orc_huffman_lengths.argtypes = [_P, C.c_int, _P]
+        L.orc_book_twoqueue_u2.restype = C.c_int
+        L.orc_book_twoqueue_u2.argtypes = [_P, C.c_int, C.c_uint32, _P, _P]
         L.orc_coarse_tune.argtypes = [_SZ, C.c_int, C.c_int, _P, _P]
         L.orc_hf_encode_u2.restype = _SZ
         L.orc_hf_encode_u2.argtypes = [_P, _SZ, _P, C.c_int, _P, _P, _P, _SZ, _P]
@@ -173,6 +175,17 @@ def codebook(hist, bklen=1024):
     book = np.zeros(bklen, np.uint32)
     rv = np.zeros(4 * 64 + 2 * bklen, np.uint8)
     nb = lib().orc_build_codebook_u2(_ptr(hist), bklen, _ptr(book), _ptr(rv))
+    assert nb == rv.size
+    return book, rv
+
+
+def book_twoqueue(hist, bklen=1024, smooth=0):
+    """The device codebook's algorithm (book_device.hh) restated: two-queue Huffman over
+    (weight, symbol)-sorted leaves of hist + smooth, reference canonisation -> (book, revbook)."""
+    hist = np.ascontiguousarray(hist, np.uint32)
+    book = np.zeros(bklen, np.uint32)
+    rv = np.zeros(4 * 64 + 2 * bklen, np.uint8)
+    nb = lib().orc_book_twoqueue_u2(_ptr(hist), bklen, smooth, _ptr(book), _ptr(rv))
     assert nb == rv.size
     return book, rv
 

@@ -1,11 +1,14 @@
 """Sampled-codebook mode (psz_amd_set_codebook(SAMPLED), brick.hip k_brick3_sample /
-k_brick3_single): the codebook comes from the histogram of every 16th brick (every brick below
-1024 bricks) plus one on every bin, and one pass predicts and packs.
+k_brick3_stream): the codebook comes from a systematic 1/16 sample of 32 x 8 x 8 units (every unit
+below 4096 units) plus one on every bin, built on the device (book_device.hh), and one streaming
+pass predicts and packs.
 
 Parity contract: quant codes, outlier set and the decompressed field equal the oracle's (the
 exact mode's) bit for bit; the Huffman segment equals the oracle encoder's output for the
-oracle-computed sampled codebook (revbook, par_nbit, every chunk's cells), with the chunks back
-to back (no gaps); the archive is an ordinary phf archive (the oracle's CPU decoder reads it).
+oracle-computed sampled codebook (the same sample of the oracle's codes, the device book's
+algorithm restated: orc_book_twoqueue_u2) -- revbook, par_nbit, every chunk's cells -- with the
+chunks back to back (no gaps); the archive is an ordinary phf archive (the oracle's CPU decoder
+reads it).
 """
 import numpy as np
 import pytest
@@ -18,21 +21,24 @@ from gpu_util import chunk_cells, d2h, empty_device, parse_archive, sync, to_dev
 pytestmark = pytest.mark.gpu
 
 
-def sampled_hist(oracle, codes, dims, bklen):
-    """Histogram of bricks 0, s, 2s, ... (brick = 256 x 8 x 8, index (bz * nby + by) * nbx + bx;
-    s = 16 from 1024 bricks up, else 1) + 1 on every bin."""
+def sampled_hist(codes, dims, bklen):
+    """Histogram of the sample units (brick.hip k_brick3_sample): units of 32 x 8 x 8, index
+    u = (uz * nuy + uy) * nux + ux; from 4096 units up every 16th, u = 16 i + i % 16, else all."""
     x, y, z = dims
-    nbx, nby, nbz = x // 256, (y + 7) // 8, (z + 7) // 8
-    nb = nbx * nby * nbz
-    stride = 16 if nb >= 64 * 16 else 1
+    nux, nuy, nuz = x // 32, (y + 7) // 8, (z + 7) // 8
+    units = nux * nuy * nuz
+    stride = 16 if units >= 256 * 16 else 1
     c = codes.reshape(z, y, x)
     h = np.zeros(bklen, np.int64)
-    for b in range(0, nb, stride):
-        bx, t = b % nbx, b // nbx
-        by, bz = t % nby, t // nby
-        blk = c[bz * 8:bz * 8 + 8, by * 8:by * 8 + 8, bx * 256:bx * 256 + 256]
+    for i in range((units + stride - 1) // stride):
+        u = i * stride + i % stride
+        if u >= units:
+            continue
+        ux, t = u % nux, u // nux
+        uy, uz = t % nuy, t // nuy
+        blk = c[uz * 8:uz * 8 + 8, uy * 8:uy * 8 + 8, ux * 32:ux * 32 + 32]
         h += np.bincount(blk.reshape(-1), minlength=bklen)[:bklen]
-    return (h + 1).astype(np.uint32)
+    return h.astype(np.uint32)
 
 
 CASES = [
@@ -44,6 +50,7 @@ CASES = [
     ((256, 32, 16), np.float32, 1e-4, True, 512, "smooth"),    # ZigZag
     ((256, 24, 16), np.float32, 1e-3, False, 64, "smooth"),    # small radius: many outliers
     ((256, 16, 16), np.float32, 1e-2, False, 512, "noise"),    # u16 rows, long codes
+    ((512, 16, 24), np.float32, 2e-3, False, 512, "noise"),    # ~10 bits/code: bricks outgrow the staging
     ((512, 128, 136), np.float32, 1e-4, False, 512, "smooth"),  # 1088 bricks: every 16th sampled
 ]
 
@@ -80,7 +87,7 @@ def test_sampled_parity(oracle, dims, dtype, eb, zz, radius, kind):
 
     # Huffman segment: the oracle's encoding with the sampled codebook, chunks back to back
     bklen = 2 * radius
-    book, rv = oracle.codebook(sampled_hist(oracle, codes_o, dims, bklen), bklen)
+    book, rv = oracle.book_twoqueue(sampled_hist(codes_o, dims, bklen), bklen, smooth=1)
     nbit_o, entry_o, bs_o, tot_o = oracle.hf_encode(codes_o, book, 256)
     np.testing.assert_array_equal(a["revbook"], rv)
     np.testing.assert_array_equal(a["par_nbit"], nbit_o)
