@@ -179,7 +179,7 @@ def lib():
 DECODER_AUTO, DECODER_LANE, DECODER_WAVE = 0, 1, 2
 # archive layout (PSZ_AMD_LAYOUT_*)
 LAYOUT_BRICK, LAYOUT_REFERENCE, LAYOUT_BRICK_FORCE = 0, 1, 2
-CODEBOOK_EXACT, CODEBOOK_SAMPLED = 0, 1
+CODEBOOK_EXACT, CODEBOOK_SAMPLED, CODEBOOK_STREAM = 0, 1, 2  # PSZ_AMD_CODEBOOK_*
 
 
 class PszError(RuntimeError):
@@ -202,8 +202,9 @@ class Resource:
                 dtype, psz_len(x, y, z), psz_pipeline(predictor, HistogramGeneric, Huffman, NullCodec),
                 C.c_void_p(stream))
         if not self._h:
-            raise PszError(PSZ_AMD_ERR_DEVICE, "psz_create_resource_manager")
+            raise PszError(L.psz_amd_last_create_status() or PSZ_AMD_ERR_DEVICE, "psz_create_resource_manager")
         self.dtype = dtype if header is None else header.dtype
+        self.codebook = CODEBOOK_SAMPLED  # the library's default (psz_amd_set_codebook)
         self.stream = int(stream or 0)  # the manager's HIP stream handle (0: the null stream)
         self.header = psz_header()
 
@@ -296,11 +297,13 @@ class Resource:
             raise PszError(st, "psz_amd_set_layout")
 
     def set_codebook(self, mode: int):
-        """CODEBOOK_EXACT (full histogram, default) or CODEBOOK_SAMPLED (every 16th brick's
-        histogram + 1, one predict+pack pass; 3-D brick fields only)."""
+        """CODEBOOK_EXACT (the reference's heap book on the host: byte-identical archives),
+        CODEBOOK_SAMPLED (default: device book, sampled for 3-D brick fields) or CODEBOOK_STREAM
+        (sampled device book + one predict/pack pass; 3-D brick fields)."""
         st = lib().psz_amd_set_codebook(self._h, int(mode))
         if st != PSZ_SUCCESS:
             raise PszError(st, "psz_amd_set_codebook")
+        self.codebook = int(mode)
 
     def decode_codes(self, d_archive: int):
         st = lib().psz_amd_decode_codes(self._h, C.c_void_p(d_archive))

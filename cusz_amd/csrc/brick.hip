@@ -2331,20 +2331,20 @@ k_brick3_stream(const T* __restrict__ in, StreamArgs a, T ebx2_r, T r)
     if (lane == 0) b = atomicAdd(a.ticket, 1u);
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
   };
-  constexpr int D = kStreamAhead<T>;
   uint32_t brick = claim();
-  T q[D][V];
+  // one y-step (the 8 z-rows of one y) in flight: loaded while the previous one is computed
+  T q[8][V];
 #pragma unroll
-  for (int j = 0; j < D; j++) ld.issue_row(brick, j, q[j]);
+  for (int z = 0; z < 8; z++) ld.issue_row(brick, z, q[z]);
   while (brick < a.nbricks) {
     const uint32_t bnext = claim();
     const uint32_t bx = brick % a.nbx, t = brick / a.nbx, by = t % a.nby, bz = t / a.nby;
     const uint32_t x0 = bx * (64 * V) + lane * V, y0 = by * 8, z0 = bz * 8;
     const uint32_t nyv = min(8u, a.ly - y0), nzv = min(8u, a.lz - z0);
-    uint32_t cnt = 0;               // outliers of the brick
-    uint32_t off = 0, fbase = 0;    // brick words packed; words [fbase, off) are in the staging
-    uint32_t xc = 0, xo = 0;        // the brick's archive offsets (known early when it flushes)
-    bool direct = false;            // (uniform) offsets taken early: flushes go straight out
+    uint32_t cnt = 0;             // outliers of the brick
+    uint32_t off = 0, fbase = 0;  // brick words packed; words [fbase, off) are in the staging
+    uint32_t xc = 0, xo = 0;      // the brick's archive offsets (known early when it flushes)
+    bool direct = false;          // (uniform) offsets taken early: flushes go straight out
     unsigned long long bbits = 0;
     uint32_t my_nbit = 0, my_loc = 0;  // lane = row: its bits and first word in the brick
     // staged words -> the archive (each lane one word per store: the offset has any alignment)
@@ -2361,22 +2361,28 @@ k_brick3_stream(const T* __restrict__ in, StreamArgs a, T ebx2_r, T r)
       fbase = off;
       hfd::wave_sync();
     };
-    T bprev[8][V], pprev[V];
+    T bprev[8][V];  // the previous y-step's z/x residuals (y-diff)
 #pragma unroll
     for (int z = 0; z < 8; z++)
 #pragma unroll
       for (int k = 0; k < V; k++) bprev[z][k] = (T)0;
 #pragma unroll 1
-    for (int r0 = 0; r0 < 64; r0 += D)
+    for (uint32_t y = 0; y < 8; y++) {
+      // phase 1, straight-line over the y-step's 8 rows: prequant, residuals in the reference
+      // order (z, x inside the 8-wide tile, y), codes; the next y-step's rows are issued as these
+      // are consumed.  Rows outside the field (partial bricks) get no codewords by selects.
+      const bool yok = y0 + y < a.ly;  // (uniform)
+      T d[8][V];
+      uint32_t qc2[8][2];  // the row's 4 codes as two u16 pairs
+      uint64_t anyol = 0;
+      T pprev[V];
 #pragma unroll
-      for (int j = 0; j < D; j++) {
-        const int row = r0 + j, z = j & 7, y = row >> 3;
+      for (int z = 0; z < 8; z++) {
         T p[V];
 #pragma unroll
-        for (int k = 0; k < V; k++) p[k] = dround(q[j][k] * ebx2_r);
-        if (row + D < 64) ld.issue_row(brick, row + D, q[j]);
-        else ld.issue_row(bnext, row + D - 64, q[j]);
-        const uint32_t gy = y0 + (uint32_t)y;
+        for (int k = 0; k < V; k++) p[k] = dround(q[z][k] * ebx2_r);
+        if (y + 1 < 8) ld.issue_row(brick, (int)(8 * (y + 1)) + z, q[z]);
+        else ld.issue_row(bnext, z, q[z]);
         T av[V];
 #pragma unroll
         for (int k = 0; k < V; k++) {
@@ -2387,54 +2393,75 @@ k_brick3_stream(const T* __restrict__ in, StreamArgs a, T ebx2_r, T r)
 #pragma unroll
         for (int k = V - 1; k > 0; k--) av[k] = av[k] - av[k - 1];
         if (x0 % 8 != 0) av[0] = av[0] - west;
-        T d[V];
+        const bool rok = yok && (uint32_t)z < nzv;
+        uint16_t c[V];
 #pragma unroll
         for (int k = 0; k < V; k++) {
-          d[k] = av[k] - bprev[z][k];
+          d[z][k] = av[k] - bprev[z][k];
           bprev[z][k] = av[k];
-        }
-        if (gy >= a.ly || z0 + (uint32_t)z >= a.lz) continue;  // outside the field (wave-uniform)
-        float olv[V];
-        uint16_t qc[V];
-        uint64_t anyol = 0;
-        uint32_t w[V], bits = 0;
-#pragma unroll
-        for (int k = 0; k < V; k++) {
           bool is_ol;
-          qc[k] = quantize<T, ZZ>(d[k], r, is_ol, olv[k]);
-          anyol |= __ballot(is_ol);
-          w[k] = s_book[qc[k]];
-          bits += w[k] >> 27;
+          float ov;
+          c[k] = quantize<T, ZZ>(d[z][k], r, is_ol, ov);
+          anyol |= __ballot(is_ol && rok);
         }
-        if (anyol) {
+        qc2[z][0] = (uint32_t)c[0] | (uint32_t)c[1] << 16;
+        qc2[z][1] = (uint32_t)c[2] | (uint32_t)c[3] << 16;
+      }
+      if (!yok) continue;  // (uniform: the whole y-step lies past the field)
+      // outliers of the y-step into the brick's slot (rare)
+      if (anyol) {
+#pragma unroll
+        for (int z = 0; z < 8; z++) {
+          if ((uint32_t)z >= nzv) break;
           uint32_t mask = 0;
+          float olv[V];
           size_t idx[V];
-          const size_t base = (size_t)(z0 + z) * plane + (size_t)gy * a.lx;
+          const size_t base = (size_t)(z0 + z) * plane + (size_t)(y0 + y) * a.lx;
 #pragma unroll
           for (int k = 0; k < V; k++) {
-            mask |= (uint32_t)(qc[k] == 0 && (ZZ ? !(dabs(d[k]) < r) : true)) << k;
+            bool is_ol;
+            const uint16_t c = quantize<T, ZZ>(d[z][k], r, is_ol, olv[k]);
+            mask |= (uint32_t)(c == 0 && is_ol) << k;
             idx[k] = base + x0 + k;
           }
-          emit_outliers<V>(a.ol, brick, cnt, mask, olv, idx);
+          if (__builtin_amdgcn_ballot_w64(mask != 0)) emit_outliers<V>(a.ol, brick, cnt, mask, olv, idx);
         }
-        const uint32_t inc = hfd::wave_incl_scan(bits);
-        const uint32_t tot = readlane(inc, 63);
-        if (off - fbase + kPackRowMax > kStageWords) {  // the staging is full: offsets now, flush
-          if (!direct) {
-            lookback(a.status, brick, lane, xc, xo, a.timeout);
-            direct = true;
-          }
-          flush();
-        }
-        const uint32_t pos = ((off - fbase) << 5) + inc - bits;
-        if (__builtin_expect(__builtin_amdgcn_ballot_w64(bits > 64u) == 0, 1))
-          hfd::pack4_or_lj(stage, pos, w, bits);
-        else
-          hfd::pack_words<V>(stage, pos, w, V);
-        if ((uint32_t)lane == (uint32_t)row) my_nbit = tot, my_loc = off;
-        off += (tot + 31) >> 5;
-        bbits += tot;
       }
+      // phase 2: codewords (LDS book), row bits by DPP scans, the y-step's size; the staging
+      // takes the offsets early and flushes when the y-step might not fit (rare)
+      uint32_t w[8][V], bits[8], inc[8], tot[8], cells = 0;
+#pragma unroll
+      for (int z = 0; z < 8; z++) {
+        const bool rok = (uint32_t)z < nzv;
+        w[z][0] = s_book[qc2[z][0] & 0xFFFFu], w[z][1] = s_book[qc2[z][0] >> 16];
+        w[z][2] = s_book[qc2[z][1] & 0xFFFFu], w[z][3] = s_book[qc2[z][1] >> 16];
+        if (!rok) w[z][0] = w[z][1] = w[z][2] = w[z][3] = 0u;
+        bits[z] = (w[z][0] >> 27) + (w[z][1] >> 27) + (w[z][2] >> 27) + (w[z][3] >> 27);
+        inc[z] = hfd::wave_incl_scan(bits[z]);
+        tot[z] = readlane(inc[z], 63);
+        cells += (tot[z] + 31) >> 5;
+      }
+      if (off - fbase + cells + 2 > (uint32_t)kStageWords) {  // the staging is full: offsets now, flush
+        if (!direct) {
+          lookback(a.status, brick, lane, xc, xo, a.timeout);
+          direct = true;
+        }
+        flush();
+      }
+      const bool wide = __builtin_amdgcn_ballot_w64(bits[0] > 64u || bits[1] > 64u || bits[2] > 64u || bits[3] > 64u ||
+                                                    bits[4] > 64u || bits[5] > 64u || bits[6] > 64u || bits[7] > 64u) != 0;
+#pragma unroll
+      for (int z = 0; z < 8; z++) {
+        const uint32_t pos = ((off - fbase) << 5) + inc[z] - bits[z];
+        if (!wide)
+          hfd::pack4_or_lj(stage, pos, w[z], bits[z]);
+        else
+          hfd::pack_words<V>(stage, pos, w[z], V);
+        if ((uint32_t)lane == 8 * y + (uint32_t)z) my_nbit = tot[z], my_loc = off;
+        off += (tot[z] + 31) >> 5;
+        bbits += tot[z];
+      }
+    }
     // the brick's place in the archive
     const uint32_t oc = min(cnt, a.ol.cap_per_brick);
     if (!direct) {

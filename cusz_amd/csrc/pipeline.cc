@@ -80,7 +80,13 @@ struct Pipeline {
   BrickLaunch bl{};               // fused brick path (brick.hip); bl.g.ok when eligible
   int layout = 0;                 // PSZ_AMD_LAYOUT_*: 0 brick layout when eligible, 1 reference layout
   bool layout_set = false;        // PSZ_AMD_LAYOUT_BRICK_FORCE: bricks also for small 2-D fields
-  int codebook = 0;               // PSZ_AMD_CODEBOOK_*: exact (full histogram) or sampled (one pass)
+  int codebook = PSZ_AMD_CODEBOOK_SAMPLED;  // PSZ_AMD_CODEBOOK_*: sampled device book (default),
+                                            // reference book (exact), streaming single pass
+  // the sampled codebook is built on a side stream, concurrently with pass 1 (the sample kernel's
+  // last workgroup builds it on the device); the encode launches wait for its event
+  hipStream_t side = nullptr;
+  hipEvent_t ev_in = nullptr, ev_book = nullptr;
+  uint32_t* d_shist = nullptr;    // sample histogram u32[kMaxBklen] + its publish ticket
   uint16_t* d_bhist = nullptr;    // per-brick u16 histograms (pass 1 -> reservation)
   uint32_t* d_ub = nullptr;       // per-brick region upper bounds (cells)
   uint32_t* d_bbase = nullptr;    // per-brick cell offsets inside their plan block
@@ -162,6 +168,10 @@ struct Pipeline {
 
   void release()
   {
+    if (ev_in) (void)hipEventDestroy(ev_in), ev_in = nullptr;
+    if (ev_book) (void)hipEventDestroy(ev_book), ev_book = nullptr;
+    if (side) (void)hipStreamDestroy(side), side = nullptr;
+    if (d_shist) (void)hipFree(d_shist), d_shist = nullptr;
     for (void* p : {(void*)d_codes, (void*)d_hist, (void*)d_book, (void*)d_slots, (void*)d_brick_cnt,
                     (void*)d_brick_off, (void*)d_spill, (void*)d_small, (void*)d_status, (void*)d_archive,
                     (void*)d_enc_temp, (void*)d_spl_slots, (void*)d_spl_cnt, (void*)d_spl_off, (void*)d_spl_x, (void*)d_spl_sps,
@@ -276,6 +286,12 @@ struct Pipeline {
     CUSZ_AMD_HIP_CHECK(hipHostMalloc(&h_xfer, kXferBytes, hipHostMallocMapped | hipHostMallocCoherent));
     std::memset(h_xfer, 0, kXferBytes);
     for (auto& e : ev) CUSZ_AMD_HIP_CHECK(hipEventCreate(&e));
+    if (bl.g.ok) {  // the sampled codebook's side stream (brick layout)
+      CUSZ_AMD_HIP_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+      CUSZ_AMD_HIP_CHECK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
+      CUSZ_AMD_HIP_CHECK(hipEventCreateWithFlags(&ev_book, hipEventDisableTiming));
+      CUSZ_AMD_HIP_CHECK(hipMalloc(&d_shist, (kMaxBklen + 16) * sizeof(uint32_t)));
+    }
     if (const char* g = getenv("CUSZ_AMD_NO_GATE")) gate = atoi(g) == 0;
     return PSZ_SUCCESS;
   }
@@ -403,6 +419,7 @@ struct Pipeline {
     int radius = 0;
     uint32_t hist_epoch = 0;  // != 0: the scan published d_hist to h_hist() with this epoch (flag 2)
     bool ext = false;         // finish with a caller's (reduced) histogram + overflow word
+    bool side_book = false;   // the sampled codebook is being built on the side stream (ev_book)
     size_t anchor_bytes = 0;
   } pend;
 
@@ -414,7 +431,7 @@ struct Pipeline {
     for (int run = 0;; run++) {
       const int g0 = grow_events;
       int s;
-      if (codebook == PSZ_AMD_CODEBOOK_SAMPLED && bl.g.ndim == 3 && use_brick(h->pipeline.predictor))
+      if (codebook == PSZ_AMD_CODEBOOK_STREAM && bl.g.ndim == 3 && use_brick(h->pipeline.predictor))
         s = compress_sampled<T>(h, in, out, outlen);
       else {
         s = compress_scan<T>(h, in, true);
@@ -437,6 +454,7 @@ struct Pipeline {
     if (broken) return PSZ_AMD_ERR_DEVICE;
     pend.active = false;
     pend.ext = false;
+    pend.side_book = false;
     const psz_predictor pred = h->pipeline.predictor;
     if (pred != Lorenzo && pred != LorenzoZigZag && pred != Spline) return PSZ_ABORT_NO_SUCH_PREDICTOR;
     if (h->pipeline.codec1 != Huffman) return PSZ_ABORT_NO_SUCH_CODEC;
@@ -493,7 +511,19 @@ struct Pipeline {
     if (brick) {
       OutlierSink bol{d_slots, d_brick_cnt, d_spill, spill_cnt(), brick_cap(), spill_cap, nullptr};
       HostPub hp;
-      if (pub_hist)
+      const bool device_book = codebook != PSZ_AMD_CODEBOOK_EXACT;
+      if (device_book && pub_hist && bl.g.ndim == 3) {
+        // a single-process compress: the codebook comes from a sample, built on the side stream
+        // while pass 1 runs (after everything the caller queued before this call)
+        CUSZ_AMD_HIP_CHECK(hipEventRecord(ev_in, stream));
+        CUSZ_AMD_HIP_CHECK(hipStreamWaitEvent(side, ev_in, 0));
+        CUSZ_AMD_HIP_CHECK((hipError_t)launch_zero(regions({{d_shist, nullptr, (size_t)(kMaxBklen + 16) * 4}}), side));
+        CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_sample<T>(bl, in, eb, radius, zz, d_shist, bklen, d_shist + kMaxBklen,
+                                                              d_book, d_archive + 176 + 128, side));
+        CUSZ_AMD_HIP_CHECK(hipEventRecord(ev_book, side));
+        pend.side_book = true;
+      }
+      if (pub_hist && !device_book)
         hp = HostPub{regions({{h_hist(), d_hist, (size_t)bklen * 4}}), const_cast<uint32_t*>(flag(2)), ++epoch,
                      hist_ticket()};
       pend.hist_epoch = hp.epoch;
@@ -532,9 +562,10 @@ struct Pipeline {
       CUSZ_AMD_HIP_CHECK((hipError_t)launch_spline3_c<T>(sa, stream));
     }
     else {
-      // the kernel's last workgroup publishes the histogram to the host (no publish launch)
+      // the kernel's last workgroup publishes the histogram to the host (no publish launch) for
+      // the host's reference codebook
       HostPub hp;
-      if (pub_hist)
+      if (pub_hist && codebook == PSZ_AMD_CODEBOOK_EXACT)
         hp = HostPub{regions({{h_hist(), d_hist, (size_t)bklen * 4}}), const_cast<uint32_t*>(flag(2)), ++epoch,
                      hist_ticket()};
       pend.hist_epoch = hp.epoch;
@@ -569,16 +600,14 @@ struct Pipeline {
     const uint32_t cap = spl ? spl_cap : cap_per_brick;
     uint32_t* spill_start = spl ? d_spl_sps : nullptr;
 
-    // codebook on the host (hf_hl.cc:21-34).  As in the brick path, every launch after the book
-    // is queued now behind a device-polled gate, and the last kernel publishes the summary: the
-    // histogram's trip to the host overlaps nothing, but no launch waits on the host's build.
-    uint32_t eh = pend.hist_epoch;  // published by the Lorenzo kernel's last workgroup, or now
-    if (!eh) {
-      eh = ++epoch;
-      CUSZ_AMD_HIP_CHECK((hipError_t)launch_publish(hist_regions(bklen), const_cast<uint32_t*>(flag(2)), eh, stream));
-    }
-    const uint32_t eg = ++gate_epoch;
-    const bool gated = gate;
+    // codebook: on the device from the full histogram (default: no host round trip), or the
+    // reference's heap on the host (PSZ_AMD_CODEBOOK_EXACT, hf_hl.cc:21-34).  On the host path,
+    // as in the brick path, every launch after the book is queued now behind a device-polled
+    // gate, and the last kernel publishes the summary: the histogram's trip to the host overlaps
+    // nothing, but no launch waits on the host's build.
+    const bool host_book = codebook == PSZ_AMD_CODEBOOK_EXACT;
+    uint32_t eh = 0, eg = 0;
+    bool gated = false;
     struct GateGuard {  // the gate opens on every path out of here (see compress_brick)
       volatile uint32_t* f;
       uint32_t e;
@@ -587,7 +616,7 @@ struct Pipeline {
       {
         if (armed) __atomic_store_n(f, e, __ATOMIC_RELEASE);
       }
-    } guard{flag(5), eg, gated};
+    } guard{flag(5), 0, false};
     auto build_book = [&]() -> int {
       int fs = wait_flag(2, eh);
       if (!fs) build_codebook(h_hist(), bklen, h_book(), h_revbook());
@@ -595,13 +624,25 @@ struct Pipeline {
       guard.armed = false;
       return fs;
     };
-    if (!gated)
-      if (int fs = build_book()) return fs;
+    if (host_book) {
+      eh = pend.hist_epoch;  // published by the Lorenzo kernel's last workgroup, or now
+      if (!eh) {
+        eh = ++epoch;
+        CUSZ_AMD_HIP_CHECK((hipError_t)launch_publish(hist_regions(bklen), const_cast<uint32_t*>(flag(2)), eh, stream));
+      }
+      eg = ++gate_epoch;
+      gated = gate;
+      guard.e = eg, guard.armed = gated;
+      if (!gated)
+        if (int fs = build_book()) return fs;
+    }
     const size_t phf_off = 176 + anchor_bytes;  // anchors: spline only (compressor.inl:160)
     const size_t rvbk = rvbk_bytes(bklen);
     const size_t nbit_rel = 128 + rvbk, entry_rel = nbit_rel + 4 * (size_t)pardeg;
     const size_t bits_rel = entry_rel + 4 * (size_t)pardeg;
-    {
+    if (!host_book)
+      CUSZ_AMD_HIP_CHECK((hipError_t)launch_book_device(d_hist, bklen, 0u, d_book, d_archive + phf_off + 128, stream));
+    else {
       const XferRegions up =
           regions({{d_book, h_book(), (size_t)bklen * 4}, {d_archive + phf_off + 128, h_revbook(), rvbk}});
       if (gated)
@@ -675,13 +716,13 @@ struct Pipeline {
     // launch after the codebook is queued NOW: the upload kernel polls a host-mapped gate word the
     // host sets once the book is built, so the encode kernels start right after it instead of
     // after the host's launch latency (and without the command processor's stream-wait latency).
-    uint32_t eh = pend.hist_epoch;  // published by the scan's last workgroup, or now
-    if (!eh) {
-      eh = ++epoch;
-      CUSZ_AMD_HIP_CHECK((hipError_t)launch_publish(hist_regions(bklen), const_cast<uint32_t*>(flag(2)), eh, stream));
-    }
-    const uint32_t eg = ++gate_epoch;
-    const bool gated = gate;
+    const size_t phf_off = 176;
+    const size_t rvbk = rvbk_bytes(bklen);
+    const size_t nbit_rel = 128 + rvbk, entry_rel = nbit_rel + 4 * (size_t)bpar;
+    const size_t bits_rel = entry_rel + 4 * (size_t)bpar;
+    const bool host_book = codebook == PSZ_AMD_CODEBOOK_EXACT;
+    uint32_t eh = 0, eg = 0;
+    bool gated = false;
     // the gate must open on every path out of here, or the stream (and every later call on
     // it) waits forever: an early error return before build_book() opens it in the destructor
     struct GateGuard {
@@ -692,7 +733,7 @@ struct Pipeline {
       {
         if (armed) __atomic_store_n(f, e, __ATOMIC_RELEASE);
       }
-    } guard{flag(5), eg, gated};
+    } guard{flag(5), 0, false};
     auto build_book = [&]() -> int {
       int fs = wait_flag(2, eh);
       if (!fs) build_codebook(h_hist(), bklen, h_book(), h_revbook());
@@ -700,13 +741,26 @@ struct Pipeline {
       guard.armed = false;
       return fs;
     };
-    if (!gated)
-      if (int fs = build_book()) return fs;
-    const size_t phf_off = 176;
-    const size_t rvbk = rvbk_bytes(bklen);
-    const size_t nbit_rel = 128 + rvbk, entry_rel = nbit_rel + 4 * (size_t)bpar;
-    const size_t bits_rel = entry_rel + 4 * (size_t)bpar;
-    {
+    if (!host_book) {
+      // device codebook, no host round trip: the sampled one from the side stream, or (a sharded
+      // finish: every rank holds the same reduced histogram) built now from the full histogram
+      if (pend.side_book)
+        CUSZ_AMD_HIP_CHECK(hipStreamWaitEvent(stream, ev_book, 0));
+      else
+        CUSZ_AMD_HIP_CHECK((hipError_t)launch_book_device(d_hist, bklen, 0u, d_book, d_archive + phf_off + 128, stream));
+      pend.side_book = false;
+    }
+    else {
+      eh = pend.hist_epoch;  // published by the scan's last workgroup, or now
+      if (!eh) {
+        eh = ++epoch;
+        CUSZ_AMD_HIP_CHECK((hipError_t)launch_publish(hist_regions(bklen), const_cast<uint32_t*>(flag(2)), eh, stream));
+      }
+      eg = ++gate_epoch;
+      gated = gate;
+      guard.e = eg, guard.armed = gated;
+      if (!gated)
+        if (int fs = build_book()) return fs;
       const XferRegions up =
           regions({{d_book, h_book(), (size_t)bklen * 4}, {d_archive + phf_off + 128, h_revbook(), rvbk}});
       if (gated)
@@ -1360,7 +1414,8 @@ int psz_amd_set_decoder(psz_resource* m, int kind)
 int psz_amd_set_codebook(psz_resource* m, int mode)
 {
   Pipeline* p = cusz_amd::P(m);
-  if (!p || (mode != PSZ_AMD_CODEBOOK_EXACT && mode != PSZ_AMD_CODEBOOK_SAMPLED)) return PSZ_AMD_ERR_INVALID_ARG;
+  if (!p || (mode != PSZ_AMD_CODEBOOK_EXACT && mode != PSZ_AMD_CODEBOOK_SAMPLED && mode != PSZ_AMD_CODEBOOK_STREAM))
+    return PSZ_AMD_ERR_INVALID_ARG;
   p->codebook = mode;
   return PSZ_SUCCESS;
 }

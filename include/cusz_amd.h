@@ -92,15 +92,22 @@ int psz_amd_set_decoder(psz_resource* m, int kind);
 #define PSZ_AMD_LAYOUT_BRICK_FORCE 2
 int psz_amd_set_layout(psz_resource* m, int layout);
 
-/* Codebook source (brick layout, 3-D fields; other fields always use EXACT).
- *  EXACT (default): the codebook of the full histogram, as the reference (compressor.inl:339-458):
- *    pass 1 predicts and counts, pass 2 packs.
- *  SAMPLED: the codebook of the histogram of every 16th brick, +1 on every bin, built before the
- *    field is predicted; one pass then predicts and packs.  Quant codes, outliers, the error bound
- *    and the decompressed field are identical to EXACT; the bitstream (and CR) differ.  The
- *    archive is an ordinary phf archive: the reference decoder reads it. */
+/* Codebook source.  Quant codes, outliers, the error bound and the decompressed field are the
+ * same in every mode; the codebook (hence the bitstream and, marginally, the CR) differs.  Every
+ * archive is an ordinary phf archive: the reference decoder reads it.
+ *  EXACT: the reference's codebook (its binary heap, hf_bk_impl1.seq.cc) of the full histogram,
+ *    built on the host (compressor.inl:339-458): the archive is byte-identical to the reference
+ *    encoder's output for the same codes and chunking.
+ *  SAMPLED (default): a canonical Huffman codebook built on the DEVICE (book_device.hh: two-queue
+ *    construction, the same total bits as the heap's on the same histogram), no host round trip.
+ *    3-D brick fields: from a systematic 1/16 sample of the field (+1 per bin), built on a side
+ *    stream while pass 1 runs; every other field (and a sharded finish, from the reduced
+ *    histogram): from the full histogram.
+ *  STREAM (3-D brick fields): the sampled codebook, then ONE pass predicts and packs (k_brick3_
+ *    stream: no code buffer, no gaps between bricks); experimental. */
 #define PSZ_AMD_CODEBOOK_EXACT 0
 #define PSZ_AMD_CODEBOOK_SAMPLED 1
+#define PSZ_AMD_CODEBOOK_STREAM 2
 int psz_amd_set_codebook(psz_resource* m, int mode);
 
 /* ---- sharded compress (multi-GPU; the reference has no multi-GPU path) ----

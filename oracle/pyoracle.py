@@ -190,6 +190,28 @@ def book_twoqueue(hist, bklen=1024, smooth=0):
     return book, rv
 
 
+def sample_histogram(codes, dims, bklen=1024):
+    """The sampled-codebook histogram (cusz_amd/csrc/brick.hip k_brick3_sample): units of
+    32 x 8 x 8 elements (four 8^3 Lorenzo tiles), unit u = (uz * nuy + uy) * nux + ux; from 4096
+    units up every 16th unit, u = 16 i + i % 16 (cycling through the x positions), else every
+    unit; the quant codes of the unit's in-field elements are counted."""
+    x, y, z = dims
+    nux, nuy, nuz = x // 32, (y + 7) // 8, (z + 7) // 8
+    units = nux * nuy * nuz
+    stride = 16 if units >= 256 * 16 else 1
+    c = np.asarray(codes).reshape(z, y, x)
+    h = np.zeros(bklen, np.int64)
+    for i in range((units + stride - 1) // stride):
+        u = i * stride + i % stride
+        if u >= units:
+            continue
+        ux, t = u % nux, u // nux
+        uy, uz = t % nuy, t // nuy
+        blk = c[uz * 8:uz * 8 + 8, uy * 8:uy * 8 + 8, ux * 32:ux * 32 + 32]
+        h += np.bincount(blk.reshape(-1), minlength=bklen)[:bklen]
+    return h.astype(np.uint32)
+
+
 def huffman_lengths(hist, bklen=1024):
     hist = np.ascontiguousarray(hist, np.uint32)
     lens = np.zeros(bklen, np.uint8)
@@ -244,13 +266,14 @@ def phf_header_bytes(bklen, sublen, pardeg, original_len, total_nbit, total_ncel
     return b
 
 
-def phf_segment(codes, bklen=1024, sublen=None, n_cu=256):
-    """The Huffman segment of an archive (hf_buf.cc:111-139,191-211)."""
+def phf_segment(codes, bklen=1024, sublen=None, n_cu=256, books=None):
+    """The Huffman segment of an archive (hf_buf.cc:111-139,191-211); books = (book, revbook)
+    to encode with instead of the reference's codebook of the full histogram."""
     n = codes.size
     if sublen is None:
         sublen, _ = coarse_tune(n, n_cu)
     hist = histogram(codes, bklen)
-    book, rv = codebook(hist, bklen)
+    book, rv = books if books is not None else codebook(hist, bklen)
     nbit, entry, bs, tot = hf_encode(codes, book, sublen)
     pardeg = nbit.size
     sizes = [PHF_FORCED_ALIGN, rv.size, 4 * pardeg, 4 * pardeg, 4 * bs.size]

@@ -3,6 +3,8 @@ import ctypes as C
 
 import numpy as np
 
+import cusz_amd as cz
+
 _hip = None
 
 
@@ -79,6 +81,18 @@ def chunk_cells(par_nbit, par_entry, bitstream):
     covered = np.zeros(bitstream.size, bool)
     covered[idx] = True
     return bitstream[idx], ~covered
+
+
+def expected_books(oracle, r, codes, dims, bklen, layout):
+    """The codebook a compress used (psz_amd_set_codebook): EXACT -> the reference's heap book of
+    the full histogram; SAMPLED (default) / STREAM -> the device book (two-queue, restated by
+    orc_book_twoqueue_u2) of the sample + 1 per bin (3-D brick fields) or of the full histogram."""
+    if r.codebook == cz.CODEBOOK_EXACT:
+        return oracle.codebook(oracle.histogram(codes, bklen), bklen)
+    x, y, z = (tuple(dims) + (1, 1))[:3]
+    if layout == cz.LAYOUT_BRICK and z > 1:
+        return oracle.book_twoqueue(oracle.sample_histogram(codes, (x, y, z), bklen), bklen, smooth=1)
+    return oracle.book_twoqueue(oracle.histogram(codes, bklen), bklen, smooth=0)
 
 
 def check_phf_against_oracle(a, info, seg_o, layout):

@@ -30,6 +30,8 @@ def test_nyx_six_fields_sharded_equals_whole(bound):
     st = torch.cuda.current_stream().cuda_stream
     res = [cz.Resource(cz.F4, s.dims, stream=st) for s in slabs]
     whole = cz.Resource(cz.F4, FULL, stream=st)
+    for r in res + [whole]:  # the reference codebook on both sides (the single compress samples otherwise)
+        r.set_codebook(cz.CODEBOOK_EXACT)
     out = torch.empty(FULL[0] * FULL[1] * FULL[2], dtype=torch.float32, device="cuda")
     hists = torch.zeros((WORLD, 1025), dtype=torch.int32, device="cuda")
     mm = torch.empty((WORLD, 2), dtype=torch.float64, device="cuda")

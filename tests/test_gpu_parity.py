@@ -13,7 +13,7 @@ import pytest
 
 import cusz_amd as cz
 from cusz_amd import datagen
-from gpu_util import check_phf_against_oracle, d2h, empty_device, parse_archive, sync, to_device
+from gpu_util import check_phf_against_oracle, d2h, expected_books, empty_device, parse_archive, sync, to_device
 
 pytestmark = pytest.mark.gpu
 
@@ -33,7 +33,7 @@ def _field(kind, dims, dtype, seed):
 
 
 def run_roundtrip(oracle, data, dims, eb, dtype=np.float32, zigzag=False, radius=512, sublen=0,
-                  check_bound=True, layout=None):
+                  check_bound=True, layout=None, codebook=None):
     n = int(np.prod(dims))
     tdt = "float32" if dtype == np.float32 else "float64"
     import torch
@@ -44,6 +44,8 @@ def run_roundtrip(oracle, data, dims, eb, dtype=np.float32, zigzag=False, radius
         r.set_sublen(sublen)
     if layout is not None:
         r.set_layout(layout)
+    if codebook is not None:
+        r.set_codebook(codebook)
     d_in = to_device(data)
     ptr, nbytes, st = r.compress(d_in.data_ptr(), eb, cz.Abs, radius)
     arch = d2h(ptr, nbytes).tobytes()
@@ -71,7 +73,8 @@ def run_roundtrip(oracle, data, dims, eb, dtype=np.float32, zigzag=False, radius
     bklen = 2 * radius
     hist_g = d2h(ino.d_hist, 4 * bklen, np.uint32)
     np.testing.assert_array_equal(hist_g, oracle.histogram(codes_o, bklen))
-    seg_o, info = oracle.phf_segment(codes_o, bklen, sublen=a["sublen"])
+    books = expected_books(oracle, r, codes_o, dims, bklen, ino.layout)
+    seg_o, info = oracle.phf_segment(codes_o, bklen, sublen=a["sublen"], books=books)
     check_phf_against_oracle(a, info, seg_o, ino.layout)
 
     # ---- stage 3: decompress into an un-zeroed, NaN-poisoned buffer, with each decoder -----
@@ -130,6 +133,20 @@ CASES = [
 def test_parity_vs_oracle(oracle, kind, dims, dtype, eb, zigzag, radius):
     data = _field(kind, dims, dtype, seed=sum(dims))
     run_roundtrip(oracle, data, dims, eb, dtype, zigzag, radius)
+
+
+EXACT_CASES = [c for c in CASES if c[1] in ((512, 256, 24), (3600, 1800, 1), (200_003, 1, 1), (130, 70, 30),
+                                            (64, 64, 64))]
+
+
+@pytest.mark.parametrize("kind,dims,dtype,eb,zigzag,radius", EXACT_CASES,
+                         ids=[f"{c[0]}-{'x'.join(map(str, c[1]))}-{np.dtype(c[2]).name}-zz{int(c[4])}" for c in EXACT_CASES])
+def test_parity_exact_reference_book(oracle, kind, dims, dtype, eb, zigzag, radius):
+    """PSZ_AMD_CODEBOOK_EXACT: the reference's heap codebook of the full histogram, built on the
+    host -- the Huffman segment equals the reference encoder's (byte for byte on the reference
+    layout, chunk for chunk on the brick layout)."""
+    data = _field(kind, dims, dtype, seed=sum(dims))
+    run_roundtrip(oracle, data, dims, eb, dtype, zigzag, radius, codebook=cz.CODEBOOK_EXACT)
 
 
 @pytest.mark.parametrize("sublen", [256, 1024, 4096])

@@ -16,22 +16,24 @@ from gpu_util import d2h, sync, to_device
 pytestmark = pytest.mark.gpu
 
 
-def _whole(data, dims, eb, dtype, layout, sublen):
+def _whole(data, dims, eb, dtype, layout, sublen, codebook=cz.CODEBOOK_EXACT):
     r = cz.Resource(cz.F4 if dtype == np.float32 else cz.F8, dims)
     r.set_layout(layout)
+    r.set_codebook(codebook)
     if sublen:
         r.set_sublen(sublen)
     ptr, nb, _ = r.compress(to_device(data).data_ptr(), eb)
     return d2h(ptr, nb).tobytes(), r
 
 
-def _sharded(data, dims, world, eb, dtype, layout, sublen):
+def _sharded(data, dims, world, eb, dtype, layout, sublen, codebook=cz.CODEBOOK_EXACT):
     slabs = [s for s in plan_slabs(dims, world) if s.count]
     res, dins = [], []
     hists = torch.zeros((len(slabs), 1025), dtype=torch.int32, device="cuda")  # + the overflow word
     for i, s in enumerate(slabs):
         r = cz.Resource(cz.F4 if dtype == np.float32 else cz.F8, s.dims)
         r.set_layout(layout)
+        r.set_codebook(codebook)
         if sublen:
             r.set_sublen(sublen)
         d = to_device(data[s.offset:s.offset + s.count])
@@ -71,11 +73,34 @@ def test_sharded_merge_equals_whole_field(dims, world, dtype, layout, sublen):
     assert err <= 1.001 * eb
 
 
+@pytest.mark.parametrize("dims,world,layout", [((256, 32, 40), 3, cz.LAYOUT_BRICK),
+                                               ((256, 32, 40), 3, cz.LAYOUT_REFERENCE),
+                                               ((100_000, 1, 1), 2, cz.LAYOUT_BRICK)])
+def test_sharded_device_book(dims, world, layout):
+    """The default codebook mode on the sharded path: every rank builds the same device book from
+    the reduced histogram (no host round trip).  The merged archive decompresses within the bound,
+    and equals a single compress that also books the full histogram (reference layout, 1-D)."""
+    x, y, z = dims
+    data = (datagen.smooth3d_np(dims, 5) if z > 1 else datagen.hacc1d_np(x, 5)).astype(np.float32)
+    eb = 1e-4
+    merged = _sharded(data, dims, world, eb, np.float32, layout, 0, codebook=cz.CODEBOOK_SAMPLED)
+    single, r = _whole(data, dims, eb, np.float32, layout, 0, codebook=cz.CODEBOOK_SAMPLED)
+    if layout == cz.LAYOUT_REFERENCE or z == 1:
+        assert merged == single
+    d_arch = torch.frombuffer(bytearray(merged), dtype=torch.uint8).cuda()
+    out = torch.full((data.size,), float("nan"), dtype=torch.float32, device="cuda")
+    r.decompress(d_arch.data_ptr(), len(merged), out.data_ptr())
+    sync()
+    err = np.abs(out.cpu().numpy().astype(np.float64) - data.astype(np.float64)).max()
+    assert err <= 1.001 * eb + 2.0 ** -23 * float(np.abs(data).max())
+
+
 def test_scan_then_finish_equals_compress():
     dims = (256, 24, 16)
     data = datagen.smooth3d_np(dims, 7)
     single, _ = _whole(data, dims, 1e-4, np.float32, cz.LAYOUT_BRICK, 0)
     r = cz.Resource(cz.F4, dims)
+    r.set_codebook(cz.CODEBOOK_EXACT)
     d = to_device(data)
     h = torch.zeros(1025, dtype=torch.int32, device="cuda")
     r.compress_scan(d.data_ptr(), 1e-4, h.data_ptr())
