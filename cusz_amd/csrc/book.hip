@@ -13,7 +13,7 @@ __global__ void __launch_bounds__(hbook::kThreads) k_book(const uint32_t* hist, 
                                                            uint32_t* book, uint8_t* revbook)
 {
   __shared__ hbook::Smem sm;
-  hbook::build(hist, bklen, smooth, book, revbook, sm);
+  hbook::build<hbook::kThreads>(hist, bklen, smooth, book, revbook, sm);
 }
 
 }  // namespace

@@ -210,11 +210,24 @@ __device__ __forceinline__ void store_brick_row(const BrickCodes& bcs, uint16_t*
   }
 }
 
+// Pass-1 visiting order (BrickSample): iteration j < count takes sample brick j stride + stride / 2,
+// then the other bricks in index order (the k-th of them: group k / (stride - 1), skipping the
+// group's sample position; stride - 1 is a power of two).  stride 1: index order.
+__device__ __forceinline__ uint32_t pass1_brick(uint32_t j, const BrickSample& sp)
+{
+  if (sp.stride <= 1) return j;
+  const uint32_t o = sp.stride / 2;
+  if (j < sp.count) return j * sp.stride + o;
+  const uint32_t k = j - sp.count, m = sp.stride - 2, g = k >> (31 - __builtin_clz(sp.stride - 1)), p = k & m;
+  return g * sp.stride + (p < o ? p : p + 1);
+}
+
 // End of a pass-1 unit: outlier count, row mask, the unit's histogram as a u16 record (16-B
-// stores, 8 bins per lane; the wave's LDS copy is cleared) and into the workgroup histogram.
+// stores, 8 bins per lane; the wave's LDS copy is cleared) and into the workgroup histogram; a
+// sample brick also adds it to the codebook sample (global atomics) and then counts itself done.
 __device__ __forceinline__ void finish_unit(const OutlierSink& ol, const BrickCodes& bcs, uint32_t u, uint32_t cnt,
                                             uint64_t rowmask, uint32_t* s_hist, uint32_t* s_wg, uint16_t* bhist,
-                                            int hs, int lane)
+                                            int hs, int lane, const BrickSample& sp, bool sample)
 {
   if (lane == 0) ol.brick_cnt[u] = cnt;
   if (lane == 0) bcs.rowmask[u] = rowmask;  // kUnitBricks == 1: unit = brick
@@ -235,8 +248,26 @@ __device__ __forceinline__ void finish_unit(const OutlierSink& ol, const BrickCo
 #pragma unroll
     for (int k = 0; k < 8; k++)
       if (c[k]) atomicAdd(&s_wg[i0 + k], c[k]);
+    if (sample)
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        if (c[k]) atomicAdd(&sp.hist[(i0 + k) * kSampleBinStride], c[k]);
   }
   hfd::wave_sync();
+  if (sample) {
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's sample atomics have completed
+    uint32_t prev = 0;
+    if (lane == 0) prev = __hip_atomic_fetch_add(sp.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((uint32_t)__builtin_amdgcn_readfirstlane((int)prev) == sp.count - 1 && sp.pub_flag) {
+      // the sample is complete: this wave hands it to the host (agent-scope reads: every
+      // sample brick's atomics have completed before its count)
+      for (int i = lane; i < sp.bklen; i += 64)
+        sp.pub_dst[i] = __hip_atomic_load(sp.hist + i * kSampleBinStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence_system();
+      hfd::wave_sync();
+      if (lane == 0) __hip_atomic_store(sp.pub_flag, sp.pub_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 // =========================================================================================
@@ -256,10 +287,10 @@ constexpr int kScanAhead = sizeof(T) == 4 ? CUSZ_AMD_SCAN_AHEAD : 8;
 
 template <typename T, int V, bool ZZ>
 __global__ void __launch_bounds__(64 * kBrickWaves)
-__attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? 4 : 1)))  // f32: <= 128 VGPRs, 4 waves per SIMD
+__attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? 3 : 1)))  // f32: <= 168 VGPRs, 3 waves per SIMD
 k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T ebx2_r, T r, OutlierSink ol,
               uint32_t* __restrict__ g_hist, uint16_t* __restrict__ bhist, BrickCodes bcs, int bklen,
-              uint32_t nbx, uint32_t nby, uint32_t nbricks, HostPub pub)
+              uint32_t nbx, uint32_t nby, uint32_t nbricks, HostPub pub, BrickSample sp)
 {
   extern __shared__ uint32_t smem[];
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wid: uniform (SGPR)
@@ -276,18 +307,19 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
   const int hs = bhist_stride(bklen);
   constexpr int D = kScanAhead<T>;
   static_assert(64 % D == 0 && D % 8 == 0, "the queue holds whole y-steps");
-  uint32_t u = blockIdx.x * kBrickWaves + wid;
+  uint32_t it = blockIdx.x * kBrickWaves + wid;  // iteration; its brick in the pass-1 order (BrickSample)
   const T bias = r - (T)bcs.c0;  // the byte-first path (below)
   T q[D][V];
 #pragma unroll
-  for (int j = 0; j < D; j++) ld.issue_row(u * kUnitBricks, j, q[j]);
+  for (int j = 0; j < D; j++) ld.issue_row(it < nunits ? pass1_brick(it, sp) : nbricks, j, q[j]);
   static_assert(kUnitBricks == 1, "one row mask per unit");
   uint64_t rowmask = 0;  // rows of the brick stored as u16 (uniform)
-  for (; u < nunits; u += nw) {
+  for (; it < nunits; it += nw) {
     uint32_t cnt = 0;
-    const uint32_t bend = min((u + 1) * kUnitBricks, nbricks);
-    for (uint32_t brick = u * kUnitBricks; brick < bend; brick++) {
-      const uint32_t bnext = brick + 1 < bend ? brick + 1 : (u + nw) * kUnitBricks;  // next brick of the stream
+    const uint32_t u = pass1_brick(it, sp);
+    const uint32_t bend = u + 1;
+    for (uint32_t brick = u; brick < bend; brick++) {
+      const uint32_t bnext = it + nw < nunits ? pass1_brick(it + nw, sp) : nbricks;  // next brick of the stream
       const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
       const uint32_t x0 = bx * (64 * V) + lane * V, y0 = by * 8, z0 = bz * 8;
       uint16_t* cbrick = bcs.c16 + (size_t)brick * 64 * (64 * V) + (size_t)lane * V;
@@ -386,7 +418,7 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
           }
         }
     }
-    finish_unit(ol, bcs, u, cnt, rowmask, s_hist, s_wg, bhist, hs, lane);
+    finish_unit(ol, bcs, u, cnt, rowmask, s_hist, s_wg, bhist, hs, lane, sp, sp.hist && it < sp.count);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < bklen; i += blockDim.x) {
@@ -409,7 +441,8 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
 template <typename T, int V, bool ZZ, int ND>
 __global__ void __launch_bounds__(64 * kBrickWaves)
 k_brick1_scan(const T* __restrict__ in, size_t n, T ebx2_r, T r, OutlierSink ol, uint32_t* __restrict__ g_hist,
-              uint16_t* __restrict__ bhist, BrickCodes bcs, int bklen, uint32_t nbricks, HostPub pub, uint32_t lx)
+              uint16_t* __restrict__ bhist, BrickCodes bcs, int bklen, uint32_t nbricks, HostPub pub, uint32_t lx,
+              BrickSample sp)
 {
   static_assert(V == 4, "W = 256");
   extern __shared__ uint32_t smem[];
@@ -461,19 +494,23 @@ k_brick1_scan(const T* __restrict__ in, size_t n, T ebx2_r, T r, OutlierSink ol,
       __builtin_memcpy(reinterpret_cast<char*>(&dst[0]) + 16 * h, &v, 16);
     }
   };
-  uint32_t u = blockIdx.x * kBrickWaves + wid;
+  uint32_t it = blockIdx.x * kBrickWaves + wid;  // iteration; its brick in the pass-1 order (BrickSample)
   T q[D][V];
   T qn[ND == 2 ? D : 1][V];
-  if constexpr (ND == 2) cursor_at(u, xi, yi);
+  {
+    const uint32_t u0 = it < nbricks ? pass1_brick(it, sp) : nbricks;
+    if constexpr (ND == 2) cursor_at(u0, xi, yi);
 #pragma unroll
-  for (int j = 0; j < D; j++) {
-    issue_row(u, j, q[j]);
-    if constexpr (ND == 2) {
-      issue_north(u, xi, yi, qn[j]);
-      advance(xi, yi);
+    for (int j = 0; j < D; j++) {
+      issue_row(u0, j, q[j]);
+      if constexpr (ND == 2) {
+        issue_north(u0, xi, yi, qn[j]);
+        advance(xi, yi);
+      }
     }
   }
-  for (; u < nbricks; u += nw) {
+  for (; it < nbricks; it += nw) {
+    const uint32_t u = pass1_brick(it, sp), un = it + nw < nbricks ? pass1_brick(it + nw, sp) : nbricks;
     uint32_t cnt = 0;
     uint64_t rowmask = 0;
     const size_t bbase = (size_t)u * kBE;
@@ -506,11 +543,11 @@ k_brick1_scan(const T* __restrict__ in, size_t n, T ebx2_r, T r, OutlierSink ol,
 #pragma unroll
           for (int k = 0; k < V; k++) p[k] = p[k] - dround(qn[j][k] * ebx2_r);
         }
-        const uint32_t bnext = row + D < 64 ? u : u + nw;
+        const uint32_t bnext = row + D < 64 ? u : un;
         if (row + D < 64) issue_row(u, row + D, q[j]);
-        else issue_row(u + nw, row + D - 64, q[j]);
+        else issue_row(un, row + D - 64, q[j]);
         if constexpr (ND == 2) {
-          if (row + D == 64) cursor_at(u + nw, xi, yi);  // the queue moves on to the next brick
+          if (row + D == 64) cursor_at(un, xi, yi);  // the queue moves on to the next brick
           issue_north(bnext, xi, yi, qn[j]);
           advance(xi, yi);
         }
@@ -548,7 +585,7 @@ k_brick1_scan(const T* __restrict__ in, size_t n, T ebx2_r, T r, OutlierSink ol,
           emit_outliers<V>(ol, u, cnt, mask, olv, idx);
         }
       }
-    finish_unit(ol, bcs, u, cnt, rowmask, s_hist, s_wg, bhist, hs, lane);
+    finish_unit(ol, bcs, u, cnt, rowmask, s_hist, s_wg, bhist, hs, lane, sp, sp.hist && it < sp.count);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < bklen; i += blockDim.x) {
@@ -2241,7 +2278,56 @@ k_brick3_sample(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz,
   for (int i = threadIdx.x; i < bklen; i += blockDim.x)
     s_h[i] = __hip_atomic_load(g_hist + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  hbook::build(s_h, bklen, 1u, book, revbook, s_book);
+  hbook::build<kSampleThreads>(s_h, bklen, 1u, book, revbook, s_book);
+}
+
+// 1-D: sample units are the reference's 1024-element tiles (lrz_c.cuhip.inl:23-109), every 16th
+// from 4096 tiles up (u = 16 i + i % 16), else every tile; lane l predicts elements [16 l, 16 l + 16)
+// of the tile (the element before a lane's first from lane l - 1, 0 at the tile start)
+__host__ __device__ inline uint32_t sample_units1(size_t n) { return (uint32_t)((n + 1023) / 1024); }
+
+template <typename T, bool ZZ>
+__global__ void __launch_bounds__(kSampleThreads)
+k_brick1_sample(const T* __restrict__ in, size_t n, T ebx2_r, T r, uint32_t* __restrict__ g_hist, int bklen,
+                uint32_t* ticket, uint32_t* book, uint8_t* revbook)
+{
+  __shared__ uint32_t s_h[kMaxBklen];
+  __shared__ hbook::Smem s_book;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (int i = threadIdx.x; i < bklen; i += blockDim.x) s_h[i] = 0;
+  __syncthreads();
+  const uint32_t units = sample_units1(n), stride = sample_stride(units), nsamp = (units + stride - 1) / stride;
+  constexpr int kW = kSampleThreads / 64;
+  for (uint32_t i = blockIdx.x * kW + wid; i < nsamp; i += gridDim.x * kW) {
+    const uint32_t u = i * stride + i % stride;
+    if (u >= units) continue;  // (uniform)
+    const size_t e0 = (size_t)u * 1024 + (size_t)lane * 16;
+    T v[16];
+#pragma unroll
+    for (int g = 0; g < 4; g++) load_row<T, 4>(in, e0, 4 * g, (uint32_t)min<size_t>(16, n > e0 ? n - e0 : 0), true,
+                                             reinterpret_cast<T(&)[4]>(v[4 * g]));
+    T p[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) p[k] = dround(v[k] * ebx2_r);
+    T west = __shfl_up(p[15], 1);
+    if (lane == 0) west = (T)0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const T d = p[k] - (k ? p[k - 1] : west);
+      bool ol;
+      float ov;
+      const uint16_t c = quantize<T, ZZ>(d, r, ol, ov);
+      if (e0 + k < n) atomicAdd(&s_h[c], 1u);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < bklen; i += blockDim.x)
+    if (s_h[i]) atomicAdd(&g_hist[i], s_h[i]);
+  if (!last_block(ticket)) return;
+  for (int i = threadIdx.x; i < bklen; i += blockDim.x)
+    s_h[i] = __hip_atomic_load(g_hist + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  hbook::build<kSampleThreads>(s_h, bklen, 1u, book, revbook, s_book);
 }
 
 __device__ __forceinline__ unsigned long long st_word(unsigned long long flag, uint32_t cells, uint32_t oc)
@@ -2530,6 +2616,17 @@ __global__ void __launch_bounds__(256) k_brick3_stream_finish(StreamArgs a, Head
 
 }  // namespace
 
+BrickSample brick_sample_plan(uint32_t nbricks, uint32_t* hist, uint32_t* done)
+{
+  BrickSample s;
+  s.hist = hist, s.done = done;
+  // stride - 1 a power of two (the order's arithmetic); >= 256 sample bricks where possible
+  s.stride = nbricks >= 4352 ? 17u : nbricks >= 2304 ? 9u : nbricks >= 1280 ? 5u : nbricks >= 768 ? 3u : 1u;
+  const uint32_t o = s.stride / 2;
+  s.count = s.stride == 1 ? nbricks : (nbricks > o ? (nbricks - o + s.stride - 1) / s.stride : 0u);
+  return s;
+}
+
 // =========================================================================================
 // host launchers
 // =========================================================================================
@@ -2591,9 +2688,9 @@ int brick_configure(BrickLaunch& L, int elem_bytes, int device)
 }
 
 template <typename T>
-int launch_brick_scan(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const OutlierSink& ol,
-                      uint32_t* hist, uint16_t* bhist, const BrickCodes& bcodes, int bklen, hipStream_t st,
-                      const HostPub& pub)
+int launch_brick_scan(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const BrickSample& sample,
+                      const OutlierSink& ol, uint32_t* hist, uint16_t* bhist, const BrickCodes& bcodes, int bklen,
+                      hipStream_t st, const HostPub& pub)
 {
   const T ebx2_r = (T)(1.0 / (eb * 2));  // lrz_c.cuhip.inl:489
   const T r = (T)radius;
@@ -2603,7 +2700,7 @@ int launch_brick_scan(const BrickLaunch& L, const T* in, double eb, int radius, 
   if (g.ndim == 1 || g.ndim == 2) {
 #define SCAN1(ZZ, ND)                                                                                           \
   k_brick1_scan<T, 4, ZZ, ND><<<grid, 64 * kBrickWaves, lds, st>>>(in, g.n, ebx2_r, r, ol, hist, bhist, bcodes, \
-                                                                   bklen, g.nbricks, pub, L.lx)
+                                                                   bklen, g.nbricks, pub, L.lx, sample)
     if (g.ndim == 1) {
       if (zz) SCAN1(true, 1); else SCAN1(false, 1);
     }
@@ -2615,10 +2712,10 @@ int launch_brick_scan(const BrickLaunch& L, const T* in, double eb, int radius, 
   }
   if (zz)
     k_brick3_scan<T, 4, true><<<grid, 64 * kBrickWaves, lds, st>>>(in, L.lx, L.ly, L.lz, ebx2_r, r, ol, hist, bhist,
-                                                                   bcodes, bklen, g.nbx, g.nby, g.nbricks, pub);
+                                                                   bcodes, bklen, g.nbx, g.nby, g.nbricks, pub, sample);
   else
     k_brick3_scan<T, 4, false><<<grid, 64 * kBrickWaves, lds, st>>>(in, L.lx, L.ly, L.lz, ebx2_r, r, ol, hist, bhist,
-                                                                    bcodes, bklen, g.nbx, g.nby, g.nbricks, pub);
+                                                                    bcodes, bklen, g.nbx, g.nby, g.nbricks, pub, sample);
   return (int)hipGetLastError();
 }
 
@@ -2658,8 +2755,19 @@ int launch_brick_sample(const BrickLaunch& L, const T* in, double eb, int radius
                         uint32_t* ticket, uint32_t* book, uint8_t* revbook, hipStream_t st)
 {
   const BrickGeom& g = L.g;
-  if (g.ndim != 3 || bklen > hbook::kThreads) return (int)hipErrorInvalidValue;
+  if ((g.ndim != 3 && g.ndim != 1) || bklen > hbook::kThreads) return (int)hipErrorInvalidValue;
   const T ebx2_r = (T)(1.0 / (eb * 2)), r = (T)radius;
+  constexpr uint32_t kW1 = kSampleThreads / 64;
+  if (g.ndim == 1) {
+    const uint32_t units1 = sample_units1(g.n), stride1 = sample_stride(units1);
+    const uint32_t ns1 = (units1 + stride1 - 1) / stride1;
+    const uint32_t grid1 = std::max(1u, std::min((ns1 + kW1 - 1) / kW1, (uint32_t)L.ncu));
+    if (zz)
+      k_brick1_sample<T, true><<<grid1, kSampleThreads, 0, st>>>(in, g.n, ebx2_r, r, hist, bklen, ticket, book, revbook);
+    else
+      k_brick1_sample<T, false><<<grid1, kSampleThreads, 0, st>>>(in, g.n, ebx2_r, r, hist, bklen, ticket, book, revbook);
+    return (int)hipGetLastError();
+  }
   const uint32_t units = sample_units(L.lx, L.ly, L.lz), stride = sample_stride(units);
   const uint32_t nsamp = (units + stride - 1) / stride;
   constexpr uint32_t kW = kSampleThreads / 64;
@@ -2811,8 +2919,9 @@ extern "C" int psz_amd_debug_brick_profile(unsigned long long* host, int reset)
 #endif
 
 #define INST(T)                                                                                                   \
-  template int launch_brick_scan<T>(const BrickLaunch&, const T*, double, int, bool, const OutlierSink&, uint32_t*, \
-                                    uint16_t*, const BrickCodes&, int, hipStream_t, const HostPub&);               \
+  template int launch_brick_scan<T>(const BrickLaunch&, const T*, double, int, bool, const BrickSample&,            \
+                                    const OutlierSink&, uint32_t*, uint16_t*, const BrickCodes&, int, hipStream_t,   \
+                                    const HostPub&);                                                                \
   template int launch_brick_decode<T>(const BrickLaunch&, const uint32_t*, size_t, const uint8_t*, int,            \
                                       const uint32_t*, const uint32_t*, T*, double, int, bool, const BrickOutliers&, \
                                       hipStream_t);

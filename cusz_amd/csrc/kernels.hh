@@ -225,6 +225,27 @@ struct BrickLaunch {
 // fills ncu and the encode-pass grids for `device`
 int brick_configure(BrickLaunch& L, int elem_bytes, int device);
 
+// The codebook sample inside pass 1 (sampled codebook mode): every `stride`-th brick (offset
+// stride / 2) is visited FIRST -- iteration j < count takes sample brick j -- and adds its
+// histogram to hist (u32[bklen], global atomics); then done (a u32) counts it, and the wave that
+// completes the sample publishes it to the host (pub_dst, then *pub_flag = pub_epoch), which
+// builds the codebook while pass 1 goes on.  hist == nullptr: no sample, bricks in index order.
+// the sample histogram's bins lie a 64-B line apart: the sample bricks finish together (first
+// round of pass 1) and their atomics would otherwise queue on the one or two memory channels of
+// a dense 4 KB array (measured: pass 1 +60 us)
+constexpr int kSampleBinStride = 16;
+struct BrickSample {
+  uint32_t* hist = nullptr;  // u32[kMaxBklen * kSampleBinStride]
+  uint32_t* done = nullptr;
+  uint32_t stride = 1, count = 0;
+  uint32_t* pub_dst = nullptr;   // host-mapped u32[bklen]
+  uint32_t* pub_flag = nullptr;  // host-mapped
+  uint32_t pub_epoch = 0;
+  int bklen = 0;
+};
+BrickSample brick_sample_plan(uint32_t nbricks, uint32_t* hist, uint32_t* done);
+
+
 // Quant codes between the two encode passes, in brick order (row r of brick b at (64 b + r) W).
 // A row whose codes all lie in [c0, c0 + 254] or are 0 (outliers) is stored as bytes (code - c0;
 // 255 for code 0) in c8; any other
@@ -238,7 +259,8 @@ struct BrickCodes {
 };
 // pass 1: predict -> global + per-brick histograms, outliers, codes in brick order
 template <typename T>
-int launch_brick_scan(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const OutlierSink& ol,
+int launch_brick_scan(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const BrickSample& sample,
+                      const OutlierSink& ol,
                       uint32_t* hist, uint16_t* bhist, const BrickCodes& bc, int bklen, hipStream_t st,
                       const HostPub& pub = HostPub{});
 // archive plan (brick.hip k_brick_plan): region sizes, cell / outlier offsets, totals, headers

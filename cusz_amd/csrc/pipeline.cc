@@ -82,11 +82,7 @@ struct Pipeline {
   bool layout_set = false;        // PSZ_AMD_LAYOUT_BRICK_FORCE: bricks also for small 2-D fields
   int codebook = PSZ_AMD_CODEBOOK_SAMPLED;  // PSZ_AMD_CODEBOOK_*: sampled device book (default),
                                             // reference book (exact), streaming single pass
-  // the sampled codebook is built on a side stream, concurrently with pass 1 (the sample kernel's
-  // last workgroup builds it on the device); the encode launches wait for its event
-  hipStream_t side = nullptr;
-  hipEvent_t ev_in = nullptr, ev_book = nullptr;
-  uint32_t* d_shist = nullptr;    // sample histogram u32[kMaxBklen] + its publish ticket
+  uint32_t* d_shist = nullptr;    // pass 1's codebook sample: strided histogram + counter
   uint16_t* d_bhist = nullptr;    // per-brick u16 histograms (pass 1 -> reservation)
   uint32_t* d_ub = nullptr;       // per-brick region upper bounds (cells)
   uint32_t* d_bbase = nullptr;    // per-brick cell offsets inside their plan block
@@ -168,9 +164,6 @@ struct Pipeline {
 
   void release()
   {
-    if (ev_in) (void)hipEventDestroy(ev_in), ev_in = nullptr;
-    if (ev_book) (void)hipEventDestroy(ev_book), ev_book = nullptr;
-    if (side) (void)hipStreamDestroy(side), side = nullptr;
     if (d_shist) (void)hipFree(d_shist), d_shist = nullptr;
     for (void* p : {(void*)d_codes, (void*)d_hist, (void*)d_book, (void*)d_slots, (void*)d_brick_cnt,
                     (void*)d_brick_off, (void*)d_spill, (void*)d_small, (void*)d_status, (void*)d_archive,
@@ -286,12 +279,8 @@ struct Pipeline {
     CUSZ_AMD_HIP_CHECK(hipHostMalloc(&h_xfer, kXferBytes, hipHostMallocMapped | hipHostMallocCoherent));
     std::memset(h_xfer, 0, kXferBytes);
     for (auto& e : ev) CUSZ_AMD_HIP_CHECK(hipEventCreate(&e));
-    if (bl.g.ok) {  // the sampled codebook's side stream (brick layout)
-      CUSZ_AMD_HIP_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
-      CUSZ_AMD_HIP_CHECK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
-      CUSZ_AMD_HIP_CHECK(hipEventCreateWithFlags(&ev_book, hipEventDisableTiming));
-      CUSZ_AMD_HIP_CHECK(hipMalloc(&d_shist, (kMaxBklen + 16) * sizeof(uint32_t)));
-    }
+    if (bl.g.ok)  // pass 1's sample: strided histogram + the done counter
+      CUSZ_AMD_HIP_CHECK(hipMalloc(&d_shist, ((size_t)kMaxBklen * kSampleBinStride + 16) * sizeof(uint32_t)));
     if (const char* g = getenv("CUSZ_AMD_NO_GATE")) gate = atoi(g) == 0;
     return PSZ_SUCCESS;
   }
@@ -419,7 +408,7 @@ struct Pipeline {
     int radius = 0;
     uint32_t hist_epoch = 0;  // != 0: the scan published d_hist to h_hist() with this epoch (flag 2)
     bool ext = false;         // finish with a caller's (reduced) histogram + overflow word
-    bool side_book = false;   // the sampled codebook is being built on the side stream (ev_book)
+    bool side_book = false;   // pass 1 publishes a codebook sample to the host (epoch: hist_epoch)
     size_t anchor_bytes = 0;
   } pend;
 
@@ -497,8 +486,10 @@ struct Pipeline {
 
     // per-call state reset (the reference never resets these: SURVEY.md Appendix B.3)
     if (brick)
-      CUSZ_AMD_HIP_CHECK((hipError_t)launch_zero(
-          regions({{d_hist, nullptr, (size_t)(bklen + 1) * 4}, {d_small, nullptr, kSmallZeroBytes}}), stream));
+      CUSZ_AMD_HIP_CHECK((hipError_t)launch_zero(regions({{d_hist, nullptr, (size_t)(bklen + 1) * 4},
+                                                          {d_small, nullptr, kSmallZeroBytes},
+                                                          {d_shist, nullptr, ((size_t)kMaxBklen * kSampleBinStride + 16) * 4}}),
+                                                 stream));
     else
       CUSZ_AMD_HIP_CHECK((hipError_t)launch_zero(regions({{d_hist, nullptr, (size_t)(bklen + 1) * 4},
                                                           {d_small, nullptr, kSmallZeroBytes},
@@ -512,22 +503,22 @@ struct Pipeline {
       OutlierSink bol{d_slots, d_brick_cnt, d_spill, spill_cnt(), brick_cap(), spill_cap, nullptr};
       HostPub hp;
       const bool device_book = codebook != PSZ_AMD_CODEBOOK_EXACT;
-      if (device_book && pub_hist && bl.g.ndim == 3) {
-        // a single-process compress: the codebook comes from a sample, built on the side stream
-        // while pass 1 runs (after everything the caller queued before this call)
-        CUSZ_AMD_HIP_CHECK(hipEventRecord(ev_in, stream));
-        CUSZ_AMD_HIP_CHECK(hipStreamWaitEvent(side, ev_in, 0));
-        CUSZ_AMD_HIP_CHECK((hipError_t)launch_zero(regions({{d_shist, nullptr, (size_t)(kMaxBklen + 16) * 4}}), side));
-        CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_sample<T>(bl, in, eb, radius, zz, d_shist, bklen, d_shist + kMaxBklen,
-                                                              d_book, d_archive + 176 + 128, side));
-        CUSZ_AMD_HIP_CHECK(hipEventRecord(ev_book, side));
-        pend.side_book = true;
+      BrickSample sample;
+      if (device_book && pub_hist && (bl.g.ndim == 3 || bl.g.ndim == 1)) {
+        // a single-process compress: pass 1 visits a sample of the bricks first, counts them into
+        // d_shist and hands the completed sample to the host, which builds the codebook (the
+        // reference's heap on sample + 1) while pass 1 goes on; the encode launches wait behind
+        // the device-polled gate as in the exact mode, but the book is ready long before
+        sample = brick_sample_plan(bl.g.nbricks, d_shist, d_shist + (size_t)kMaxBklen * kSampleBinStride);
+        sample.pub_dst = h_hist(), sample.pub_flag = const_cast<uint32_t*>(flag(2)), sample.pub_epoch = ++epoch;
+        sample.bklen = bklen;
+        pend.side_book = true;  // (the sample's epoch is pend.hist_epoch)
       }
       if (pub_hist && !device_book)
         hp = HostPub{regions({{h_hist(), d_hist, (size_t)bklen * 4}}), const_cast<uint32_t*>(flag(2)), ++epoch,
                      hist_ticket()};
-      pend.hist_epoch = hp.epoch;
-      CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_scan<T>(bl, in, eb, radius, zz, bol, d_hist, d_bhist,
+      pend.hist_epoch = pend.side_book ? sample.pub_epoch : hp.epoch;
+      CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_scan<T>(bl, in, eb, radius, zz, sample, bol, d_hist, d_bhist,
                                                           brick_codes(zz, radius), bklen, stream, hp));
       mark(2);
       pend.active = true;
@@ -720,7 +711,11 @@ struct Pipeline {
     const size_t rvbk = rvbk_bytes(bklen);
     const size_t nbit_rel = 128 + rvbk, entry_rel = nbit_rel + 4 * (size_t)bpar;
     const size_t bits_rel = entry_rel + 4 * (size_t)bpar;
-    const bool host_book = codebook == PSZ_AMD_CODEBOOK_EXACT;
+    // host book: the reference heap on the full histogram (EXACT) or on pass 1's sample + 1
+    // (SAMPLED, published mid-pass); otherwise (sharded finish, 2-D bricks) the device book
+    const bool sampled = pend.side_book;
+    const bool host_book = codebook == PSZ_AMD_CODEBOOK_EXACT || sampled;
+    pend.side_book = false;
     uint32_t eh = 0, eg = 0;
     bool gated = false;
     // the gate must open on every path out of here, or the stream (and every later call on
@@ -736,19 +731,19 @@ struct Pipeline {
     } guard{flag(5), 0, false};
     auto build_book = [&]() -> int {
       int fs = wait_flag(2, eh);
-      if (!fs) build_codebook(h_hist(), bklen, h_book(), h_revbook());
+      if (!fs) {
+        if (sampled)
+          for (int i = 0; i < bklen; i++) h_hist()[i] += 1;  // every code encodable
+        build_codebook(h_hist(), bklen, h_book(), h_revbook());
+      }
       if (gated) __atomic_store_n(flag(5), eg, __ATOMIC_RELEASE);  // always open the gate
       guard.armed = false;
       return fs;
     };
     if (!host_book) {
-      // device codebook, no host round trip: the sampled one from the side stream, or (a sharded
-      // finish: every rank holds the same reduced histogram) built now from the full histogram
-      if (pend.side_book)
-        CUSZ_AMD_HIP_CHECK(hipStreamWaitEvent(stream, ev_book, 0));
-      else
-        CUSZ_AMD_HIP_CHECK((hipError_t)launch_book_device(d_hist, bklen, 0u, d_book, d_archive + phf_off + 128, stream));
-      pend.side_book = false;
+      // device codebook, no host round trip (a sharded finish: every rank holds the same reduced
+      // histogram; 2-D bricks): built now from the full histogram
+      CUSZ_AMD_HIP_CHECK((hipError_t)launch_book_device(d_hist, bklen, 0u, d_book, d_archive + phf_off + 128, stream));
     }
     else {
       eh = pend.hist_epoch;  // published by the scan's last workgroup, or now
@@ -893,6 +888,13 @@ struct Pipeline {
 
   XferRegions readback_regions()
   {
+    // a sharded finish also reads back the summed overflow word (the device-book path sends no
+    // histogram to the host)
+    if (pend.ext)
+      return regions({{h_readback(), d_archive, 176},
+                      {h_readback() + 256, info(), sizeof(CompressInfo)},
+                      {h_readback() + 384, timeout(), 4},
+                      {h_readback() + 448, d_hist + 2 * pend.radius, 4}});
     return regions({{h_readback(), d_archive, 176},
                     {h_readback() + 256, info(), sizeof(CompressInfo)},
                     {h_readback() + 384, timeout(), 4}});

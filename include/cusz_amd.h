@@ -98,11 +98,13 @@ int psz_amd_set_layout(psz_resource* m, int layout);
  *  EXACT: the reference's codebook (its binary heap, hf_bk_impl1.seq.cc) of the full histogram,
  *    built on the host (compressor.inl:339-458): the archive is byte-identical to the reference
  *    encoder's output for the same codes and chunking.
- *  SAMPLED (default): a canonical Huffman codebook built on the DEVICE (book_device.hh: two-queue
- *    construction, the same total bits as the heap's on the same histogram), no host round trip.
- *    3-D brick fields: from a systematic 1/16 sample of the field (+1 per bin), built on a side
- *    stream while pass 1 runs; every other field (and a sharded finish, from the reduced
- *    histogram): from the full histogram.
+ *  SAMPLED (default): no host round trip on the critical path.  3-D and 1-D brick fields: pass 1
+ *    visits every 17th brick first (9th / 5th / 3rd / all for fewer bricks) and hands that
+ *    sample's histogram to the host mid-pass, which builds the reference's heap codebook of
+ *    sample + 1 per bin while pass 1 goes on.  Every other field (reference layout, 2-D bricks,
+ *    a sharded finish from the reduced histogram): a canonical Huffman codebook of the full
+ *    histogram built on the DEVICE (book_device.hh: two-queue construction, the same total bits
+ *    as the heap's on the same histogram).
  *  STREAM (3-D brick fields): the sampled codebook, then ONE pass predicts and packs (k_brick3_
  *    stream: no code buffer, no gaps between bricks); experimental. */
 #define PSZ_AMD_CODEBOOK_EXACT 0

@@ -190,17 +190,46 @@ def book_twoqueue(hist, bklen=1024, smooth=0):
     return book, rv
 
 
-def sample_histogram(codes, dims, bklen=1024):
-    """The sampled-codebook histogram (cusz_amd/csrc/brick.hip k_brick3_sample): units of
-    32 x 8 x 8 elements (four 8^3 Lorenzo tiles), unit u = (uz * nuy + uy) * nux + ux; from 4096
-    units up every 16th unit, u = 16 i + i % 16 (cycling through the x positions), else every
-    unit; the quant codes of the unit's in-field elements are counted."""
+def sample_bricks(nbricks):
+    """The codebook sample inside pass 1 (cusz_amd/csrc/brick.hip brick_sample_plan): bricks
+    j * stride + stride // 2 with stride 17 / 9 / 5 / 3 from 4352 / 2304 / 1280 / 768 bricks up,
+    else every brick."""
+    stride = 17 if nbricks >= 4352 else 9 if nbricks >= 2304 else 5 if nbricks >= 1280 else 3 if nbricks >= 768 else 1
+    if stride == 1:
+        return np.arange(nbricks)
+    b = np.arange(0, nbricks, stride) + stride // 2
+    return b[b < nbricks]
+
+
+def sample_histogram(codes, dims, bklen=1024, scheme="bricks"):
+    """The sampled codebook's histogram.
+    scheme "bricks" (PSZ_AMD_CODEBOOK_SAMPLED, brick layout): the codes of the sample bricks
+      (sample_bricks); a 3-D brick is 256 x 8 x 8 elements, index (bz * nby + by) * nbx + bx, a
+      1-D brick 16384 consecutive elements.
+    scheme "units" (PSZ_AMD_CODEBOOK_STREAM, k_brick3_sample): units of 32 x 8 x 8 elements (four
+      8^3 Lorenzo tiles), unit u = (uz * nuy + uy) * nux + ux; from 4096 units up every 16th unit,
+      u = 16 i + i % 16 (cycling through the x positions), else every unit.
+    Only in-field elements count."""
     x, y, z = dims
+    h = np.zeros(bklen, np.int64)
+    if scheme == "bricks":
+        if y == 1 and z == 1:
+            c = np.asarray(codes).reshape(-1)
+            for b in sample_bricks((x + 16383) // 16384):
+                h += np.bincount(c[b * 16384:(b + 1) * 16384], minlength=bklen)[:bklen]
+            return h.astype(np.uint32)
+        nbx, nby, nbz = x // 256, (y + 7) // 8, (z + 7) // 8
+        c = np.asarray(codes).reshape(z, y, x)
+        for b in sample_bricks(nbx * nby * nbz):
+            bx, t = b % nbx, b // nbx
+            by, bz = t % nby, t // nby
+            blk = c[bz * 8:bz * 8 + 8, by * 8:by * 8 + 8, bx * 256:bx * 256 + 256]
+            h += np.bincount(blk.reshape(-1), minlength=bklen)[:bklen]
+        return h.astype(np.uint32)
     nux, nuy, nuz = x // 32, (y + 7) // 8, (z + 7) // 8
     units = nux * nuy * nuz
     stride = 16 if units >= 256 * 16 else 1
     c = np.asarray(codes).reshape(z, y, x)
-    h = np.zeros(bklen, np.int64)
     for i in range((units + stride - 1) // stride):
         u = i * stride + i % stride
         if u >= units:

@@ -1,8 +1,9 @@
-"""Sampled codebook (psz_amd_set_codebook: SAMPLED, the default, and STREAM; brick.hip
-k_brick3_sample): the codebook comes from a systematic 1/16 sample of 32 x 8 x 8 units (every unit
-below 4096 units) plus one on every bin, built on the device (book_device.hh).  SAMPLED builds it
-on a side stream while pass 1 runs, then plans and packs as the exact mode; STREAM predicts and
-packs in one pass (k_brick3_stream).
+"""Sampled codebook (psz_amd_set_codebook: SAMPLED, the default, and STREAM): the codebook
+comes from a sample plus one on every bin, built on the device (book_device.hh).  SAMPLED: pass 1
+visits every 17th brick first (fewer bricks: 9th, 5th, 3rd, all) and a side-stream workgroup builds
+the book from their histograms while pass 1 runs, then plan and pack as the exact mode.  STREAM:
+k_brick3_sample takes a 1/16 sample of 32 x 8 x 8 units first, then one pass predicts and packs
+(k_brick3_stream).
 
 Parity contract: quant codes, outlier set and the decompressed field equal the oracle's (the
 exact mode's) bit for bit; the Huffman segment equals the oracle encoder's output for the
@@ -17,7 +18,7 @@ import torch
 
 import cusz_amd as cz
 from cusz_amd import datagen
-from gpu_util import chunk_cells, d2h, empty_device, parse_archive, sync, to_device
+from gpu_util import chunk_cells, d2h, empty_device, expected_books, parse_archive, sync, to_device
 
 pytestmark = pytest.mark.gpu
 
@@ -69,7 +70,7 @@ def test_sampled_parity(oracle, dims, dtype, eb, zz, radius, kind, mode):
 
     # Huffman segment: the oracle's encoding with the sampled codebook, chunks back to back
     bklen = 2 * radius
-    book, rv = oracle.book_twoqueue(oracle.sample_histogram(codes_o, dims, bklen), bklen, smooth=1)
+    book, rv = expected_books(oracle, r, codes_o, dims, bklen, ino.layout)
     nbit_o, entry_o, bs_o, tot_o = oracle.hf_encode(codes_o, book, 256)
     np.testing.assert_array_equal(a["revbook"], rv)
     np.testing.assert_array_equal(a["par_nbit"], nbit_o)
