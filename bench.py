@@ -515,8 +515,10 @@ def bench_field(args, world, rank, dist, dev):
             "roofline": roofline,
             "cpu_baseline": cpu,
             "e2e_host_gbps": e2e,
-            "codebook": "sampled (device-built; the reference heap book is the 'exact' mode below)"
-                        if ino.layout == cz.LAYOUT_BRICK and dims[2] > 1 and predictor != cz.Spline else "device-built",
+            "codebook": ("device two-queue book of the full histogram" if predictor == cz.Spline or sharded
+                         else "reference heap book of pass 1's brick sample + 1 (host, mid-pass)"
+                         if ino.layout == cz.LAYOUT_BRICK and (dims[2] > 1 or dims[1] == 1)
+                         else "reference heap book of the full histogram (host)"),
             "other_codebook_modes": other_modes,
             "max_abs_err": err,
         }

@@ -502,9 +502,9 @@ struct Pipeline {
     if (brick) {
       OutlierSink bol{d_slots, d_brick_cnt, d_spill, spill_cnt(), brick_cap(), spill_cap, nullptr};
       HostPub hp;
-      const bool device_book = codebook != PSZ_AMD_CODEBOOK_EXACT;
+      const bool sampled_mode = codebook != PSZ_AMD_CODEBOOK_EXACT;
       BrickSample sample;
-      if (device_book && pub_hist && (bl.g.ndim == 3 || bl.g.ndim == 1)) {
+      if (sampled_mode && pub_hist && (bl.g.ndim == 3 || bl.g.ndim == 1)) {
         // a single-process compress: pass 1 visits a sample of the bricks first, counts them into
         // d_shist and hands the completed sample to the host, which builds the codebook (the
         // reference's heap on sample + 1) while pass 1 goes on; the encode launches wait behind
@@ -514,7 +514,7 @@ struct Pipeline {
         sample.bklen = bklen;
         pend.side_book = true;  // (the sample's epoch is pend.hist_epoch)
       }
-      if (pub_hist && !device_book)
+      if (pub_hist && !pend.side_book)  // (2-D bricks: the full histogram, as in the exact mode)
         hp = HostPub{regions({{h_hist(), d_hist, (size_t)bklen * 4}}), const_cast<uint32_t*>(flag(2)), ++epoch,
                      hist_ticket()};
       pend.hist_epoch = pend.side_book ? sample.pub_epoch : hp.epoch;
@@ -554,9 +554,9 @@ struct Pipeline {
     }
     else {
       // the kernel's last workgroup publishes the histogram to the host (no publish launch) for
-      // the host's reference codebook
+      // the host's reference codebook (every mode: measured faster than the device book here)
       HostPub hp;
-      if (pub_hist && codebook == PSZ_AMD_CODEBOOK_EXACT)
+      if (pub_hist)
         hp = HostPub{regions({{h_hist(), d_hist, (size_t)bklen * 4}}), const_cast<uint32_t*>(flag(2)), ++epoch,
                      hist_ticket()};
       pend.hist_epoch = hp.epoch;
@@ -591,12 +591,14 @@ struct Pipeline {
     const uint32_t cap = spl ? spl_cap : cap_per_brick;
     uint32_t* spill_start = spl ? d_spl_sps : nullptr;
 
-    // codebook: on the device from the full histogram (default: no host round trip), or the
-    // reference's heap on the host (PSZ_AMD_CODEBOOK_EXACT, hf_hl.cc:21-34).  On the host path,
+    // codebook: the reference's heap on the host (hf_hl.cc:21-34) when the predictor's last
+    // workgroup already published the histogram (Lorenzo, single process: config 1 book stage
+    // 9 us against 46 us for the device book), else -- spline, a sharded finish -- on the device
+    // from the full histogram unless PSZ_AMD_CODEBOOK_EXACT (no host round trip).  On the host path,
     // as in the brick path, every launch after the book is queued now behind a device-polled
     // gate, and the last kernel publishes the summary: the histogram's trip to the host overlaps
     // nothing, but no launch waits on the host's build.
-    const bool host_book = codebook == PSZ_AMD_CODEBOOK_EXACT;
+    const bool host_book = codebook == PSZ_AMD_CODEBOOK_EXACT || pend.hist_epoch != 0;
     uint32_t eh = 0, eg = 0;
     bool gated = false;
     struct GateGuard {  // the gate opens on every path out of here (see compress_brick)
@@ -711,10 +713,10 @@ struct Pipeline {
     const size_t rvbk = rvbk_bytes(bklen);
     const size_t nbit_rel = 128 + rvbk, entry_rel = nbit_rel + 4 * (size_t)bpar;
     const size_t bits_rel = entry_rel + 4 * (size_t)bpar;
-    // host book: the reference heap on the full histogram (EXACT) or on pass 1's sample + 1
-    // (SAMPLED, published mid-pass); otherwise (sharded finish, 2-D bricks) the device book
+    // host book: the reference heap on the full histogram (EXACT; 2-D bricks) or on pass 1's
+    // sample + 1 (SAMPLED, published mid-pass); otherwise (a sharded finish) the device book
     const bool sampled = pend.side_book;
-    const bool host_book = codebook == PSZ_AMD_CODEBOOK_EXACT || sampled;
+    const bool host_book = codebook == PSZ_AMD_CODEBOOK_EXACT || pend.hist_epoch != 0;
     pend.side_book = false;
     uint32_t eh = 0, eg = 0;
     bool gated = false;
@@ -742,7 +744,7 @@ struct Pipeline {
     };
     if (!host_book) {
       // device codebook, no host round trip (a sharded finish: every rank holds the same reduced
-      // histogram; 2-D bricks): built now from the full histogram
+      // histogram): built now from the full histogram
       CUSZ_AMD_HIP_CHECK((hipError_t)launch_book_device(d_hist, bklen, 0u, d_book, d_archive + phf_off + 128, stream));
     }
     else {

@@ -83,12 +83,12 @@ def chunk_cells(par_nbit, par_entry, bitstream):
     return bitstream[idx], ~covered
 
 
-def expected_books(oracle, r, codes, dims, bklen, layout):
+def expected_books(oracle, r, codes, dims, bklen, layout, spline=False):
     """The codebook a compress used (psz_amd_set_codebook): EXACT -> the reference's heap book of
     the full histogram; SAMPLED (default) -> on 3-D and 1-D bricks the reference's heap book of
-    pass 1's brick sample + 1 per bin (host, mid-pass), elsewhere the device book (two-queue,
-    restated by orc_book_twoqueue_u2) of the full histogram; STREAM -> the device book of the
-    32 x 8 x 8-unit sample + 1."""
+    pass 1's brick sample + 1 per bin (host, mid-pass), for spline the device book (two-queue,
+    restated by orc_book_twoqueue_u2) of the full histogram, elsewhere the exact book;
+    STREAM -> the device book of the 32 x 8 x 8-unit sample + 1 on 3-D bricks."""
     if r.codebook == cz.CODEBOOK_EXACT:
         return oracle.codebook(oracle.histogram(codes, bklen), bklen)
     x, y, z = (tuple(dims) + (1, 1))[:3]
@@ -97,7 +97,9 @@ def expected_books(oracle, r, codes, dims, bklen, layout):
     if layout == cz.LAYOUT_BRICK and (z > 1 or y == 1):  # 3-D and 1-D bricks sample inside pass 1
         # the reference's heap on sample + 1, built on the host while pass 1 goes on
         return oracle.codebook(oracle.sample_histogram(codes, (x, y, z), bklen) + np.uint32(1), bklen)
-    return oracle.book_twoqueue(oracle.histogram(codes, bklen), bklen, smooth=0)
+    if spline:
+        return oracle.book_twoqueue(oracle.histogram(codes, bklen), bklen, smooth=0)
+    return oracle.codebook(oracle.histogram(codes, bklen), bklen)
 
 
 def check_phf_against_oracle(a, info, seg_o, layout):

@@ -50,7 +50,7 @@ def _roundtrip(oracle, dims, dtype, eb, mode=cz.Abs, seed=5):
     np.testing.assert_array_equal(a["ol_val"].view(np.uint32), ov_o.view(np.uint32))
     np.testing.assert_array_equal(d2h(ino.d_hist, 4096, np.uint32), oracle.histogram(codes_o))
     seg_o, _ = oracle.phf_segment(codes_o, 1024, sublen=a["sublen"],
-                                  books=expected_books(oracle, r, codes_o, dims, 1024, ino.layout))
+                                  books=expected_books(oracle, r, codes_o, dims, 1024, ino.layout, spline=True))
     assert a["phf"] == seg_o
     out = empty_device(n, torch.float32 if dtype == np.float32 else torch.float64)
     out.fill_(float("nan"))
