@@ -20,3 +20,5 @@ for x in stats fetch write; do
 done
 python3 scripts/prof_summary.py $tag $d/stats $d/fetch $d/write > $d/summary.txt && cp profiles/${tag}_summary.json profiles/pmc_config$cfg.json && cat $d/summary.txt
 mkdir -p gpurun_out/profiles_out && cp profiles/${tag}_* profiles/pmc_config$cfg.json gpurun_out/profiles_out/
+# the raw traces stay on the box (gpurun_out is copied back only under 64 MiB)
+cp $d/summary.txt gpurun_out/profiles_out/${tag}_summary.txt && rm -rf $d
