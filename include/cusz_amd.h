@@ -156,7 +156,8 @@ const char* psz_amd_version(void);
 /* The device codebook (no host round trip; NOT the reference's heap order, the same total bit
  * count): canonical Huffman book (u32[bklen]) and reverse book (4 * 64 + 2 * bklen bytes) of the
  * device histogram IN_d_hist (+ smooth per bin: 1 makes every symbol encodable), all device
- * pointers, on `stream`.  bklen <= 1024.  The sampled-codebook mode builds its book this way. */
+ * pointers, on `stream`.  bklen <= 1024.  Spline fields, sharded finishes and the stream mode build
+ * their book this way. */
 int psz_amd_build_book_device(const uint32_t* IN_d_hist, int bklen, uint32_t smooth, uint32_t* OUT_d_book,
                               uint8_t* OUT_d_revbook, void* stream);
 
