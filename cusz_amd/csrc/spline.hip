@@ -23,6 +23,7 @@
 #include <algorithm>
 
 #include "common.hh"
+#include "hf_device.hh"
 #include "kernels.hh"
 
 namespace cusz_amd {
@@ -152,6 +153,29 @@ __device__ void spl_interpolate(T* s, int* e, const TileInfo& t, float eb_r0, fl
   __syncthreads();
 }
 
+// The tiles a persistent workgroup walks: blocks b and b + 8 share an XCD (dispatch is
+// round-robin; used for speed only), so block b takes the it-th tile of XCD range b % 8 -- each
+// XCD works through one contiguous eighth of the tiles, and tiles that share +1 faces are read
+// through the same L2.  Any grid that is not a multiple of 8 walks tile = b + it * grid.
+struct TileOrder {
+  uint32_t hi, first, step;
+  __device__ TileOrder(uint32_t n)
+  {
+    if (gridDim.x % 8u == 0u && gridDim.x >= 8u) {
+      const uint32_t per = (n + 7u) / 8u, lo = min((blockIdx.x & 7u) * per, n);
+      hi = min(lo + per, n), first = lo + (blockIdx.x >> 3), step = gridDim.x >> 3;
+    }
+    else
+      hi = n, first = blockIdx.x, step = gridDim.x;
+  }
+  // tile of iteration it, or ~0u past the last
+  __device__ uint32_t at(uint32_t it) const
+  {
+    const uint64_t t = (uint64_t)first + (uint64_t)it * step;
+    return t < hi ? (uint32_t)t : ~0u;
+  }
+};
+
 __device__ __forceinline__ TileInfo tile_of(uint32_t tile, uint32_t gdx, uint32_t gdy, uint32_t gdz, uint32_t X,
                                             uint32_t Y, uint32_t Z)
 {
@@ -193,8 +217,9 @@ __global__ void __launch_bounds__(kSplThreads, 4) k_spline3_c(SplineArgs<T> a)
       pv[k] = v;
     }
   };
-  if (blockIdx.x < a.ntiles) fetch(blockIdx.x);
-  for (uint32_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+  const TileOrder order(a.ntiles);
+  if (order.at(0) != ~0u) fetch(order.at(0));
+  for (uint32_t it = 0, tile = order.at(0); tile != ~0u; tile = order.at(++it)) {
     const TileInfo t = tile_of(tile, a.gdx, a.gdy, a.gdz, X, Y, Z);
     // scratch: data of the 33x9x9 region (0 outside the field), anchor codes = radius
 #pragma unroll
@@ -213,7 +238,7 @@ __global__ void __launch_bounds__(kSplThreads, 4) k_spline3_c(SplineArgs<T> a)
       const uint32_t gx = t.bx * 32 + 8 * tid, gy = t.by * 8, gz = t.bz * 8;
       if (gx < X && gy < Y && gz < Z) a.anchor[gx / 8 + ax * (gy / 8 + (size_t)ay * (gz / 8))] = s_data[sidx(8 * tid, 0, 0)];
     }
-    if (tile + gridDim.x < a.ntiles) fetch(tile + gridDim.x);
+    if (order.at(it + 1) != ~0u) fetch(order.at(it + 1));
     spl_interpolate<T, true>(s_data, s_code, t, a.eb_r, a.ebx2, radius);
     // interior codes out (shmem2global_32x8x8data_with_compaction, spline3.inl:370-398): plane z
     // of the tile per pass, thread -> (x, y).  Outliers get their (z, y, x) rank from a count
@@ -221,40 +246,42 @@ __global__ void __launch_bounds__(kSplThreads, 4) k_spline3_c(SplineArgs<T> a)
     const int px = tid & 31, py = tid >> 5;
     const uint32_t gx = t.bx * 32 + px, gy = t.by * 8 + py;
     uint32_t mine = 0;  // bit z: this thread's point of plane z is an outlier
-    for (int z = 0; z < 8; z++) {
+    const size_t gid0 = gx + (size_t)X * (gy + (size_t)Y * (t.bz * 8));
+    const size_t plane = (size_t)X * Y;
+    for (int z = 0; z < 8; z++) {  // codes and histogram; outliers counted per (plane, wave)
       const int cand = s_code[sidx(px, py, z)];
-      const bool ol = gx < X && gy < Y && t.bz * 8 + z < Z && !(cand >= 0 && cand < 2 * radius);
+      const bool in = gx < X && gy < Y && t.bz * 8 + z < Z;
+      const bool q = cand >= 0 && cand < 2 * radius;
+      if (in) {
+        a.codes[gid0 + z * plane] = q ? (uint16_t)cand : (uint16_t)0;
+        atomicAdd(&s_hist[q ? cand : 0], 1u);
+      }
+      const bool ol = in && !q;
       const uint64_t m = __ballot(ol);
       if (lane == 0) s_pc[z][wid] = (uint32_t)__popcll(m);
       mine |= (uint32_t)ol << z;
     }
     __syncthreads();
-    if (tid == 0) {
-      uint32_t run = 0;
-      for (int z = 0; z < 8; z++)
-        for (int w = 0; w < 4; w++) {
-          const uint32_t c = s_pc[z][w];
-          s_pc[z][w] = run;
-          run += c;
-        }
-      s_sp = run > a.ol.cap_per_brick ? atomicAdd(a.ol.spill_cnt, run - a.ol.cap_per_brick) : 0u;
-      a.ol.brick_cnt[tile] = run;
-      if (run > a.ol.cap_per_brick) a.ol.spill_start[tile] = s_sp;
+    if (wid == 0) {  // exclusive offsets in (z, wave) order: one DPP scan over the 32 counts
+      uint32_t* pc = &s_pc[0][0];
+      const uint32_t c = lane < 32 ? pc[lane] : 0u;
+      const uint32_t inc = hfd::wave_incl_scan(c);
+      if (lane < 32) pc[lane] = inc - c;
+      const uint32_t run = (uint32_t)__builtin_amdgcn_readlane((int)inc, 31);
+      if (lane == 0) {
+        s_sp = run > a.ol.cap_per_brick ? atomicAdd(a.ol.spill_cnt, run - a.ol.cap_per_brick) : 0u;
+        a.ol.brick_cnt[tile] = run;
+        if (run > a.ol.cap_per_brick) a.ol.spill_start[tile] = s_sp;
+      }
     }
     __syncthreads();
     uint64_t* slot = a.ol.slots + (size_t)tile * a.ol.cap_per_brick;
-    for (int z = 0; z < 8; z++) {
-      const uint32_t gz = t.bz * 8 + z;
-      const bool in = gx < X && gy < Y && gz < Z;
-      const int cand = s_code[sidx(px, py, z)];
-      const bool q = cand >= 0 && cand < 2 * radius;
-      const size_t gid = gx + (size_t)X * (gy + (size_t)Y * gz);
-      if (in) {
-        a.codes[gid] = q ? (uint16_t)cand : (uint16_t)0;
-        atomicAdd(&s_hist[q ? cand : 0], 1u);
-      }
+    for (int z = 0; z < 8; z++) {  // outlier cells at their (z, y, x) rank
       const uint64_t m = __ballot((mine >> z) & 1u);
+      if (!m) continue;
       if ((mine >> z) & 1u) {
+        const int cand = s_code[sidx(px, py, z)];
+        const size_t gid = gid0 + z * plane;
         const uint32_t pos = s_pc[z][wid] + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
         const uint64_t cell = make_cell((float)cand, (uint32_t)gid);
@@ -383,7 +410,7 @@ __global__ void __launch_bounds__(kSplThreads, 4) k_spline3_x(SplineXArgs<T> a)
   uint32_t pcv[kEnt], pgid[kEnt], pm = 0;
   auto ranges_of = [&](uint32_t tile, uint32_t& r0, uint32_t& r1) {
     r0 = r1 = 0;
-    if (!bk || tid >= 8 || tile >= a.ntiles) return;
+    if (!bk || tid >= 8 || tile == ~0u) return;
     const TileInfo t = tile_of(tile, a.gdx, a.gdy, a.gdz, X, Y, Z);
     const uint32_t nbx = t.bx + (tid & 1), nby = t.by + ((tid >> 1) & 1), nbz = t.bz + (tid >> 2);
     if (nbx < a.gdx && nby < a.gdy && nbz < a.gdz) {
@@ -391,7 +418,7 @@ __global__ void __launch_bounds__(kSplThreads, 4) k_spline3_x(SplineXArgs<T> a)
       r0 = a.boff[nt], r1 = a.boff[nt + 1];
     }
   };
-  auto fetch = [&](uint32_t tile) {
+  auto fetch = [&](uint32_t tile, uint32_t after) {
     const TileInfo t = tile_of(tile, a.gdx, a.gdy, a.gdz, X, Y, Z);
     const int ot = opaque(tid);  // recomputed per fetch, not hoisted into live registers
 #pragma unroll
@@ -408,7 +435,7 @@ __global__ void __launch_bounds__(kSplThreads, 4) k_spline3_x(SplineXArgs<T> a)
       const uint32_t Ax = tid % 5 + t.bx * 4, Ay = (tid / 5) % 2 + t.by, Az = tid / 10 + t.bz;
       if (Ax < ax && Ay < ay && Az < az) pa = a.anchor[Ax + ax * (Ay + (size_t)ay * Az)];
     }
-    ranges_of(tile + gridDim.x, pr0, pr1);
+    ranges_of(after, pr0, pr1);
   };
   // entry e of the concatenated ranges of buffer `buf` -> its cell index (false past the end)
   auto locate = [&](int buf, uint32_t e, uint32_t& j) {
@@ -446,14 +473,15 @@ __global__ void __launch_bounds__(kSplThreads, 4) k_spline3_x(SplineXArgs<T> a)
       s_code[sidx(lx, ly, lz)] = (int)__builtin_bit_cast(float, cv);
   };
   int par = 0;
-  if (blockIdx.x < a.ntiles) {
-    ranges_of(blockIdx.x, pr0, pr1);
+  const TileOrder order(a.ntiles);
+  if (order.at(0) != ~0u) {
+    ranges_of(order.at(0), pr0, pr1);
     if (tid < 8) s_rng[0][tid][0] = pr0, s_rng[0][tid][1] = pr1;
-    fetch(blockIdx.x);
+    fetch(order.at(0), order.at(1));
     __syncthreads();
     if (bk) entries(0);
   }
-  for (uint32_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x, par ^= 1) {
+  for (uint32_t it = 0, tile = order.at(0); tile != ~0u; tile = order.at(++it), par ^= 1) {
     const TileInfo t = tile_of(tile, a.gdx, a.gdy, a.gdz, X, Y, Z);
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
@@ -481,15 +509,21 @@ __global__ void __launch_bounds__(kSplThreads, 4) k_spline3_x(SplineXArgs<T> a)
       }
       if (total) __syncthreads();
     }
-    if (tile + gridDim.x < a.ntiles) {
-      fetch(tile + gridDim.x);
+    if (order.at(it + 1) != ~0u) {
+      fetch(order.at(it + 1), order.at(it + 2));
       if (bk) entries(par ^ 1);
     }
     spl_interpolate<T, false>(s_data, s_code, t, a.eb_r, a.ebx2, radius);
-    for (int z = 0; z < 8; z++) {
+    {
       const int x = tid & 31, y = tid >> 5;
-      const uint32_t gx = t.bx * 32 + x, gy = t.by * 8 + y, gz = t.bz * 8 + z;
-      if (gx < X && gy < Y && gz < Z) a.out[gx + (size_t)X * (gy + (size_t)Y * gz)] = s_data[sidx(x, y, z)];
+      const uint32_t gx = t.bx * 32 + x, gy = t.by * 8 + y;
+      T* o = a.out + (gx + (size_t)X * (gy + (size_t)Y * (t.bz * 8)));
+      const size_t plane = (size_t)X * Y;
+      const uint32_t nz = min(8u, Z - t.bz * 8);
+      if (gx < X && gy < Y)
+#pragma unroll
+        for (int z = 0; z < 8; z++)
+          if ((uint32_t)z < nz) o[z * plane] = s_data[sidx(x, y, z)];
     }
     __syncthreads();
   }
