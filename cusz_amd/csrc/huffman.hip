@@ -199,9 +199,11 @@ constexpr int kGatherTile = 64;
 
 // (and, when total_nbit is set, the archive's bit total: one 64-bit atomic per tile, so the
 // finalize step needs no summing launch of its own)
+// (per-tile bit totals go to tile_bits and k_hf_tile_scan sums them: one atomic per tile on the
+// single total_nbit word queued 2,048 waves at the L2 -- 27 us for config 5's 131,072 chunks)
 __global__ void __launch_bounds__(256) k_hf_tile_sums(const uint32_t* __restrict__ par_nbit, int pardeg,
-                                                      uint32_t* __restrict__ tile_sum, int ntiles,
-                                                      unsigned long long* total_nbit)
+                                                      uint32_t* __restrict__ tile_sum, uint32_t* __restrict__ tile_bits,
+                                                      int ntiles)
 {
   const int lane = threadIdx.x & 63;
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -214,26 +216,28 @@ __global__ void __launch_bounds__(256) k_hf_tile_sums(const uint32_t* __restrict
   }
   acc = wave_sum(acc);
   bits = wave_sum(bits);
-  if (lane == 0) {
-    tile_sum[t] = acc;
-    if (total_nbit) atomicAdd(total_nbit, (unsigned long long)bits);
-  }
+  if (lane == 0) tile_sum[t] = acc, tile_bits[t] = bits;
 }
 
 // exclusive scan of the tile totals in place (one workgroup; ntiles <= 1024 * 8)
-__global__ void __launch_bounds__(1024) k_hf_tile_scan(uint32_t* __restrict__ tile_sum, int ntiles)
+__global__ void __launch_bounds__(1024) k_hf_tile_scan(uint32_t* __restrict__ tile_sum,
+                                                      const uint32_t* __restrict__ tile_bits, int ntiles,
+                                                      unsigned long long* total_nbit)
 {
   __shared__ uint32_t s_wave[16];
   __shared__ uint32_t s_carry;
+  __shared__ unsigned long long s_bits[16];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if (tid == 0) s_carry = 0;
   __syncthreads();
+  unsigned long long bits = 0;  // this thread's share of the total bit count
   for (int base = 0; base < ntiles; base += 1024 * 8) {
     uint32_t v[8], sum = 0;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const int i = base + tid * 8 + k;
       v[k] = i < ntiles ? tile_sum[i] : 0u;
+      bits += i < ntiles ? tile_bits[i] : 0u;
       sum += v[k];
     }
     const uint32_t inc = wave_incl_scan(sum, lane);
@@ -252,6 +256,16 @@ __global__ void __launch_bounds__(1024) k_hf_tile_scan(uint32_t* __restrict__ ti
     __syncthreads();
     if (tid == 0) s_carry = tot;
     __syncthreads();
+  }
+  if (!total_nbit) return;
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) bits += __shfl_xor(bits, d);
+  if (lane == 0) s_bits[wid] = bits;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < 16; w++) t += s_bits[w];
+    *total_nbit = t;
   }
 }
 
@@ -878,7 +892,7 @@ int hf_encode_groups(int sublen, int pardeg)
   return (pardeg + kEncW - 1) / kEncW;
 }
 
-static size_t hf_encode_tile_words(int pardeg) { return ((size_t)pardeg + kGatherTile - 1) / kGatherTile + 4; }
+static size_t hf_encode_tile_words(int pardeg) { return 2 * (((size_t)pardeg + kGatherTile - 1) / kGatherTile) + 4; }
 
 size_t hf_encode_temp_words(int sublen, int pardeg)
 {  // chunk slots at a worst-case stride, then the per-tile cell totals
@@ -903,8 +917,9 @@ int launch_hf_encode(const HfEncodeArgs& a, hipStream_t st)
   k_hf_pack<<<grid, 64 * kPackWaves, lds, st>>>(a, cellcap);
   const int ntiles = (a.pardeg + kGatherTile - 1) / kGatherTile;
   uint32_t* tile_sum = a.temp + hf_encode_temp_words(a.sublen, a.pardeg) - hf_encode_tile_words(a.pardeg);
-  k_hf_tile_sums<<<(ntiles + 3) / 4, 256, 0, st>>>(a.par_nbit, a.pardeg, tile_sum, ntiles, a.total_nbit);
-  k_hf_tile_scan<<<1, 1024, 0, st>>>(tile_sum, ntiles);
+  uint32_t* tile_bits = tile_sum + ntiles;
+  k_hf_tile_sums<<<(ntiles + 3) / 4, 256, 0, st>>>(a.par_nbit, a.pardeg, tile_sum, tile_bits, ntiles);
+  k_hf_tile_scan<<<1, 1024, 0, st>>>(tile_sum, tile_bits, ntiles, a.total_nbit);
   k_hf_gather<<<ntiles, 256, 0, st>>>(a, cellcap, tile_sum);
   return (int)hipGetLastError();
 }

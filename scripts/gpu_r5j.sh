@@ -1,4 +1,4 @@
 #!/bin/bash
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_spline.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/tall.log 2>&1; rc=$?; tail -3 gpurun_out/tall.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/tall.log 2>&1; rc=$?; tail -3 gpurun_out/tall.log; [ $rc -eq 0 ] || exit $rc
 scripts/ab_spl.sh
