@@ -68,6 +68,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (PCIe) path timing")
     ap.add_argument("--profile-only", action="store_true", help="few steps, no baselines (rocprof)")
+    ap.add_argument("--no-other-modes", action="store_true", help="skip the other codebook modes' timings")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the launch, rank plumbing and the collectives (gloo) only")
     return ap.parse_args()
@@ -402,7 +403,8 @@ def bench_field(args, world, rank, dist, dev):
     # archives to the reference encoder's; its histogram goes to the host and the book comes back
     # behind a device-polled gate), STREAM = the sampled device codebook + one predict/pack pass
     other_modes = None
-    if world == 1 and ino.layout == cz.LAYOUT_BRICK and dims[1] > 1 and dims[2] > 1 and predictor != cz.Spline:
+    if (world == 1 and not args.no_other_modes and ino.layout == cz.LAYOUT_BRICK and dims[1] > 1 and dims[2] > 1
+            and predictor != cz.Spline):
         other_modes = {}
         for name, mode in (("exact", cz.CODEBOOK_EXACT), ("stream", cz.CODEBOOK_STREAM)):
             r.set_codebook(mode)
@@ -516,7 +518,7 @@ def bench_field(args, world, rank, dist, dev):
             "cpu_baseline": cpu,
             "e2e_host_gbps": e2e,
             "codebook": ("device two-queue book of the full histogram" if predictor == cz.Spline or sharded
-                         else "reference heap book of pass 1's brick sample + 1 (host, mid-pass)"
+                         else "two-queue book of pass 1's brick sample + 1 (host, mid-pass)"
                          if ino.layout == cz.LAYOUT_BRICK and (dims[2] > 1 or dims[1] == 1)
                          else "reference heap book of the full histogram (host)"),
             "other_codebook_modes": other_modes,

@@ -298,8 +298,9 @@ class Resource:
 
     def set_codebook(self, mode: int):
         """CODEBOOK_EXACT (the reference's heap book on the host: byte-identical archives),
-        CODEBOOK_SAMPLED (default: device book, sampled for 3-D brick fields) or CODEBOOK_STREAM
-        (sampled device book + one predict/pack pass; 3-D brick fields)."""
+        CODEBOOK_SAMPLED (default: 3-D and 1-D bricks book pass 1's brick sample on the host with
+        the two-queue algorithm; spline / sharded finishes build the book on the device) or
+        CODEBOOK_STREAM (sampled device book + one predict/pack pass; 3-D brick fields)."""
         st = lib().psz_amd_set_codebook(self._h, int(mode))
         if st != PSZ_SUCCESS:
             raise PszError(st, "psz_amd_set_codebook")

@@ -145,12 +145,12 @@ int huffman_code_lengths(const uint32_t* hist, int bklen, uint8_t* len)
   return deepest;
 }
 
-// book: u32[bklen]; revbook: 4*64 + 2*bklen bytes.  Returns revbook bytes.
-int build_codebook(const uint32_t* hist, int bklen, uint32_t* book, uint8_t* revbook)
-{
-  std::vector<uint8_t> len(bklen);
-  const int max_l = huffman_code_lengths(hist, bklen, len.data());
+namespace {
 
+// canonical codes from lengths (hf_canon.seq.cc:105-161): book words code | len << 27, revbook
+// = first[32] | entry[32] | symbols by (length, symbol).  Returns revbook bytes.
+int canonize(const uint8_t* len, int max_l, int bklen, uint32_t* book, uint8_t* revbook)
+{
   int32_t numl[32] = {0}, first[32] = {0}, entry[32] = {0}, next[32];
   for (int s = 0; s < bklen; s++)
     if (len[s]) numl[len[s]]++;
@@ -162,7 +162,7 @@ int build_codebook(const uint32_t* hist, int bklen, uint32_t* book, uint8_t* rev
   }
   first[0] = 0xff;
 
-  std::vector<uint16_t> keys(bklen, 0);
+  uint16_t keys[kMaxSym] = {0};
   for (int s = 0; s < bklen; s++) book[s] = 0xFFFFFFFFu;
   for (int s = 0; s < bklen; s++) {
     const int l = len[s];
@@ -175,8 +175,97 @@ int build_codebook(const uint32_t* hist, int bklen, uint32_t* book, uint8_t* rev
   std::memset(revbook, 0, bytes);
   std::memcpy(revbook, first, 128);
   std::memcpy(revbook + 128, entry, 128);
-  std::memcpy(revbook + 256, keys.data(), 2 * bklen);
+  std::memcpy(revbook + 256, keys, 2 * bklen);
   return bytes;
+}
+
+// Two-queue Huffman code lengths (the device builder's algorithm, book_device.hh; oracle
+// orc_book_twoqueue_u2): weights w = hist + smooth, used symbols stably sorted by weight (an LSD
+// radix sort on (weight << 10 | symbol): no data-dependent branches), then at each merge the two
+// smallest heads of the leaf queue and the internal-node queue (internal weights never
+// decrease), a leaf before an internal node of equal weight.  A tree deeper than kLmax halves
+// every weight ((w + 1) / 2) and is rebuilt.  Any such tree is optimal for the weights: the
+// sampled codebook needs an optimal code, not the reference's heap order, and this takes a
+// few microseconds where the heap's data-dependent sift branches cost 20-60 us per call on the
+// benchmark host (cold branch predictor, one build per compress).
+int twoqueue_lengths(const uint64_t* w, int bklen, uint8_t* len)
+{
+  uint64_t key[kMaxSym], tmp[kMaxSym];
+  int n = 0;
+  uint64_t wmax = 0;
+  for (int s = 0; s < bklen; s++)
+    if (w[s]) key[n++] = w[s] << 10 | (uint64_t)s, wmax = std::max(wmax, w[s]);
+  std::memset(len, 0, bklen);
+  if (n == 0) return 0;
+  if (n == 1) {
+    len[key[0] & 1023] = 1;
+    return 1;
+  }
+  // LSD radix sort, 11-bit digits, over the bits the keys use
+  int bits = 10;
+  while (bits < 64 && (wmax << 10) >> bits) bits++;
+  uint64_t* a = key;
+  uint64_t* b = tmp;
+  for (int sh = 0; sh < bits; sh += 11) {
+    uint32_t cnt[2048 + 1] = {0};
+    for (int i = 0; i < n; i++) cnt[((a[i] >> sh) & 2047) + 1]++;
+    for (int d = 0; d < 2048; d++) cnt[d + 1] += cnt[d];
+    for (int i = 0; i < n; i++) b[cnt[(a[i] >> sh) & 2047]++] = a[i];
+    std::swap(a, b);
+  }
+  uint64_t iw[kMaxSym];
+  int16_t par[2 * kMaxSym];
+  int li = 0, ii = 0, ni = 0;
+  while ((n - li) + (ni - ii) > 1) {
+    int pick[2];
+    uint64_t pw[2];
+    for (int k = 0; k < 2; k++) {
+      const uint64_t lw = li < n ? a[li] >> 10 : ~0ull, nw = ii < ni ? iw[ii] : ~0ull;
+      const bool leaf = li < n && lw <= nw;
+      pick[k] = leaf ? li : n + ii;
+      pw[k] = leaf ? lw : nw;
+      li += leaf, ii += !leaf;
+    }
+    par[pick[0]] = par[pick[1]] = (int16_t)(n + ni);
+    iw[ni++] = pw[0] + pw[1];
+  }
+  uint8_t depth[2 * kMaxSym];
+  const int root = n + ni - 1;
+  int maxl = 0;
+  depth[root] = 0;
+  for (int id = root - 1; id >= 0; id--) {
+    const int d = std::min(depth[par[id]] + 1, 255);
+    depth[id] = (uint8_t)d;
+    if (id < n) {
+      len[a[id] & 1023] = (uint8_t)d;
+      maxl = std::max(maxl, d);
+    }
+  }
+  return maxl;
+}
+
+}  // namespace
+
+// book: u32[bklen]; revbook: 4*64 + 2*bklen bytes.  Returns revbook bytes.
+int build_codebook(const uint32_t* hist, int bklen, uint32_t* book, uint8_t* revbook)
+{
+  std::vector<uint8_t> len(bklen);
+  const int max_l = huffman_code_lengths(hist, bklen, len.data());
+  return canonize(len.data(), max_l, bklen, book, revbook);
+}
+
+// the two-queue book of hist + smooth (see twoqueue_lengths); the device builder's output
+int build_codebook_twoqueue(const uint32_t* hist, int bklen, uint32_t smooth, uint32_t* book, uint8_t* revbook)
+{
+  if (bklen <= 0 || bklen > kMaxSym) return -1;
+  uint64_t w[kMaxSym];
+  uint8_t len[kMaxSym];
+  for (int s = 0; s < bklen; s++) w[s] = (uint64_t)hist[s] + smooth;
+  int max_l;
+  while ((max_l = twoqueue_lengths(w, bklen, len)) > kLmax)
+    for (int s = 0; s < bklen; s++)
+      if (w[s]) w[s] = (w[s] + 1) / 2;
+  return canonize(len, max_l, bklen, book, revbook);
 }
 
 }  // namespace cusz_amd

@@ -32,6 +32,7 @@
 namespace cusz_amd {
 
 int build_codebook(const uint32_t* hist, int bklen, uint32_t* book, uint8_t* revbook);
+int build_codebook_twoqueue(const uint32_t* hist, int bklen, uint32_t smooth, uint32_t* book, uint8_t* revbook);
 int hf_encode_groups(int sublen, int pardeg);
 size_t hf_encode_temp_words(int sublen, int pardeg);
 
@@ -507,7 +508,7 @@ struct Pipeline {
       if (sampled_mode && pub_hist && (bl.g.ndim == 3 || bl.g.ndim == 1)) {
         // a single-process compress: pass 1 visits a sample of the bricks first, counts them into
         // d_shist and hands the completed sample to the host, which builds the codebook (the
-        // reference's heap on sample + 1) while pass 1 goes on; the encode launches wait behind
+        // two-queue book of sample + 1) while pass 1 goes on; the encode launches wait behind
         // the device-polled gate as in the exact mode, but the book is ready long before
         sample = brick_sample_plan(bl.g.nbricks, d_shist, d_shist + (size_t)kMaxBklen * kSampleBinStride);
         sample.pub_dst = h_hist(), sample.pub_flag = const_cast<uint32_t*>(flag(2)), sample.pub_epoch = ++epoch;
@@ -713,8 +714,9 @@ struct Pipeline {
     const size_t rvbk = rvbk_bytes(bklen);
     const size_t nbit_rel = 128 + rvbk, entry_rel = nbit_rel + 4 * (size_t)bpar;
     const size_t bits_rel = entry_rel + 4 * (size_t)bpar;
-    // host book: the reference heap on the full histogram (EXACT; 2-D bricks) or on pass 1's
-    // sample + 1 (SAMPLED, published mid-pass); otherwise (a sharded finish) the device book
+    // host book: the reference heap on the full histogram (EXACT; 2-D bricks) or the two-queue
+    // book of pass 1's sample + 1 (SAMPLED, published mid-pass); otherwise (a sharded finish) the
+    // device book
     const bool sampled = pend.side_book;
     const bool host_book = codebook == PSZ_AMD_CODEBOOK_EXACT || pend.hist_epoch != 0;
     pend.side_book = false;
@@ -734,9 +736,10 @@ struct Pipeline {
     auto build_book = [&]() -> int {
       int fs = wait_flag(2, eh);
       if (!fs) {
-        if (sampled)
-          for (int i = 0; i < bklen; i++) h_hist()[i] += 1;  // every code encodable
-        build_codebook(h_hist(), bklen, h_book(), h_revbook());
+        if (sampled)  // two-queue book of sample + 1 (every code encodable; codebook.cc)
+          build_codebook_twoqueue(h_hist(), bklen, 1u, h_book(), h_revbook());
+        else
+          build_codebook(h_hist(), bklen, h_book(), h_revbook());
       }
       if (gated) __atomic_store_n(flag(5), eg, __ATOMIC_RELEASE);  // always open the gate
       guard.armed = false;

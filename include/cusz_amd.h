@@ -100,11 +100,12 @@ int psz_amd_set_layout(psz_resource* m, int layout);
  *    encoder's output for the same codes and chunking.
  *  SAMPLED (default): no host round trip on the critical path.  3-D and 1-D brick fields: pass 1
  *    visits every 17th brick first (9th / 5th / 3rd / all for fewer bricks) and hands that
- *    sample's histogram to the host mid-pass, which builds the reference's heap codebook of
- *    sample + 1 per bin while pass 1 goes on.  Every other field (reference layout, 2-D bricks,
- *    a sharded finish from the reduced histogram): a canonical Huffman codebook of the full
- *    histogram built on the DEVICE (book_device.hh: two-queue construction, the same total bits
- *    as the heap's on the same histogram).
+ *    sample's histogram to the host mid-pass, which builds the two-queue Huffman codebook of
+ *    sample + 1 per bin while pass 1 goes on (the device builder's algorithm, run on the host).
+ *    Reference layout and 2-D bricks: the EXACT book of the full histogram (published by the
+ *    predictor's last workgroup).  Spline fields and a sharded finish (reduced histogram): the
+ *    two-queue codebook of the full histogram built on the DEVICE (book_device.hh; the same
+ *    total bits as the heap's on the same histogram).
  *  STREAM (3-D brick fields): the sampled codebook, then ONE pass predicts and packs (k_brick3_
  *    stream: no code buffer, no gaps between bricks); experimental. */
 #define PSZ_AMD_CODEBOOK_EXACT 0

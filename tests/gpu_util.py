@@ -85,9 +85,9 @@ def chunk_cells(par_nbit, par_entry, bitstream):
 
 def expected_books(oracle, r, codes, dims, bklen, layout, spline=False):
     """The codebook a compress used (psz_amd_set_codebook): EXACT -> the reference's heap book of
-    the full histogram; SAMPLED (default) -> on 3-D and 1-D bricks the reference's heap book of
-    pass 1's brick sample + 1 per bin (host, mid-pass), for spline the device book (two-queue,
-    restated by orc_book_twoqueue_u2) of the full histogram, elsewhere the exact book;
+    the full histogram; SAMPLED (default) -> on 3-D and 1-D bricks the two-queue book (restated by
+    orc_book_twoqueue_u2) of pass 1's brick sample + 1 per bin (built on the host mid-pass), for
+    spline the two-queue book of the full histogram (device), elsewhere the exact book;
     STREAM -> the device book of the 32 x 8 x 8-unit sample + 1 on 3-D bricks."""
     if r.codebook == cz.CODEBOOK_EXACT:
         return oracle.codebook(oracle.histogram(codes, bklen), bklen)
@@ -95,8 +95,8 @@ def expected_books(oracle, r, codes, dims, bklen, layout, spline=False):
     if r.codebook == cz.CODEBOOK_STREAM and layout == cz.LAYOUT_BRICK and z > 1:
         return oracle.book_twoqueue(oracle.sample_histogram(codes, (x, y, z), bklen, "units"), bklen, smooth=1)
     if layout == cz.LAYOUT_BRICK and (z > 1 or y == 1):  # 3-D and 1-D bricks sample inside pass 1
-        # the reference's heap on sample + 1, built on the host while pass 1 goes on
-        return oracle.codebook(oracle.sample_histogram(codes, (x, y, z), bklen) + np.uint32(1), bklen)
+        # the two-queue book of sample + 1, built on the host while pass 1 goes on
+        return oracle.book_twoqueue(oracle.sample_histogram(codes, (x, y, z), bklen), bklen, smooth=1)
     if spline:
         return oracle.book_twoqueue(oracle.histogram(codes, bklen), bklen, smooth=0)
     return oracle.codebook(oracle.histogram(codes, bklen), bklen)

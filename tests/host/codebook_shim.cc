@@ -5,9 +5,16 @@
 
 namespace cusz_amd {
 int build_codebook(const uint32_t* hist, int bklen, uint32_t* book, uint8_t* revbook);
+int build_codebook_twoqueue(const uint32_t* hist, int bklen, uint32_t smooth, uint32_t* book, uint8_t* revbook);
 }
 
 extern "C" int shim_build_codebook(const uint32_t* hist, int bklen, uint32_t* book, uint8_t* revbook)
 {
   return cusz_amd::build_codebook(hist, bklen, book, revbook);
+}
+
+extern "C" int shim_build_codebook_twoqueue(const uint32_t* hist, int bklen, uint32_t smooth, uint32_t* book,
+                                            uint8_t* revbook)
+{
+  return cusz_amd::build_codebook_twoqueue(hist, bklen, smooth, book, revbook);
 }

@@ -1,6 +1,7 @@
-"""The library's host codebook builder (cusz_amd/csrc/codebook.cc, compiled here with g++ from
-the same source the library links) against the oracle's independent builder (psz_oracle.c):
-identical book words and revbook bytes, including trees deeper than 27 bits (length limit).
+"""The library's host codebook builders (cusz_amd/csrc/codebook.cc, compiled here with g++ from
+the same source the library links) against the oracle's independent builders (psz_oracle.c):
+identical book words and revbook bytes, including trees deeper than 27 bits (length limit) --
+the reference heap (exact mode) and the two-queue book of hist + smooth (sampled bricks).
 CPU-only."""
 import ctypes as C
 import os
@@ -24,6 +25,8 @@ def shim(tmp_path_factory):
     lib = C.CDLL(str(out))
     lib.shim_build_codebook.restype = C.c_int
     lib.shim_build_codebook.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+    lib.shim_build_codebook_twoqueue.restype = C.c_int
+    lib.shim_build_codebook_twoqueue.argtypes = [C.c_void_p, C.c_int, C.c_uint32, C.c_void_p, C.c_void_p]
     return lib
 
 
@@ -58,3 +61,18 @@ def test_host_codebook_matches_oracle(shim, oracle):
         np.testing.assert_array_equal(rv, orv)
         deep += int((book[book != 0xFFFFFFFF] >> 27).max(initial=0) == 27)
     assert deep > 0  # the length limit was exercised
+
+
+def test_host_twoqueue_matches_oracle(shim, oracle):
+    deep = 0
+    for t, (bklen, h) in enumerate(_hists()):
+        smooth = t % 2
+        book = np.zeros(bklen, np.uint32)
+        rv = np.zeros(4 * 64 + 2 * bklen, np.uint8)
+        nb = shim.shim_build_codebook_twoqueue(h.ctypes.data, bklen, smooth, book.ctypes.data, rv.ctypes.data)
+        obook, orv = oracle.book_twoqueue(h, bklen, smooth=smooth)
+        assert nb == orv.size
+        np.testing.assert_array_equal(book, obook)
+        np.testing.assert_array_equal(rv, orv)
+        deep += int((book[book != 0xFFFFFFFF] >> 27).max(initial=0) == 27)
+    assert deep > 0
