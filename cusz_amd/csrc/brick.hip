@@ -1748,9 +1748,14 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
       pcell[k] = ranked && j < x.ce ? make_uint2(ol.cells[2 * (size_t)j], ol.cells[2 * (size_t)j + 1]) : make_uint2(0, 0);
     }
   };
-  Next nx = fetch(blockIdx.x * (blockDim.x >> 6) + wid);
+  // a wave's first brick: 8 consecutive bricks per workgroup (they share par_nbit / par_entry /
+  // bitstream lines in one L2), unless the field has fewer bricks than waves (a small slab): then
+  // wave w of every workgroup takes brick w * grid + block, spreading them over every CU (one per
+  // SIMD for 1024 bricks) instead of filling half the CUs two waves per SIMD
+  const uint32_t b0 = nbricks <= nw ? (uint32_t)wid * gridDim.x + blockIdx.x : blockIdx.x * (blockDim.x >> 6) + wid;
+  Next nx = fetch(b0);
   prefetch(nx);
-  for (uint32_t brick = blockIdx.x * (blockDim.x >> 6) + wid; brick < nbricks; brick += nw) {
+  for (uint32_t brick = b0; brick < nbricks; brick += nw) {
     BPROF(pc[0]++; tp = __builtin_readcyclecounter();)
     const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
     const uint32_t y0 = by * 8, z0 = bz * 8;
