@@ -99,7 +99,7 @@ int psz_amd_set_layout(psz_resource* m, int layout);
  *    built on the host (compressor.inl:339-458): the archive is byte-identical to the reference
  *    encoder's output for the same codes and chunking.
  *  SAMPLED (default): no host round trip on the critical path.  3-D and 1-D brick fields: pass 1
- *    visits every 17th brick first (9th / 5th / 3rd / all for fewer bricks) and hands that
+ *    visits every 33rd brick first (17th / 9th / 5th / 3rd / all for fewer bricks) and hands that
  *    sample's histogram to the host mid-pass, which builds the two-queue Huffman codebook of
  *    sample + 1 per bin while pass 1 goes on (the device builder's algorithm, run on the host).
  *    Reference layout and 2-D bricks: the EXACT book of the full histogram (published by the

@@ -192,9 +192,10 @@ def book_twoqueue(hist, bklen=1024, smooth=0):
 
 def sample_bricks(nbricks):
     """The codebook sample inside pass 1 (cusz_amd/csrc/brick.hip brick_sample_plan): bricks
-    j * stride + stride // 2 with stride 17 / 9 / 5 / 3 from 4352 / 2304 / 1280 / 768 bricks up,
-    else every brick."""
-    stride = 17 if nbricks >= 4352 else 9 if nbricks >= 2304 else 5 if nbricks >= 1280 else 3 if nbricks >= 768 else 1
+    j * stride + stride // 2 with stride 33 / 17 / 9 / 5 / 3 from 8192 / 4352 / 2304 / 1280 / 768
+    bricks up, else every brick."""
+    stride = (33 if nbricks >= 8192 else 17 if nbricks >= 4352 else 9 if nbricks >= 2304 else 5 if nbricks >= 1280
+              else 3 if nbricks >= 768 else 1)
     if stride == 1:
         return np.arange(nbricks)
     b = np.arange(0, nbricks, stride) + stride // 2
