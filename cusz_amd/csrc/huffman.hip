@@ -19,6 +19,7 @@
 #include "common.hh"
 #include "hf_device.hh"
 #include "kernels.hh"
+#include "pub_device.hh"
 
 namespace cusz_amd {
 
@@ -108,7 +109,18 @@ __device__ __forceinline__ void load_codes16(const uint16_t* p, int mine, uint32
 //  (2) k_hf_chunk_scan: one workgroup scans the per-chunk cell counts into par_entry;
 //  (3) k_hf_gather: one wave per chunk copies its cells to their final place (coalesced).
 // The extra 2 x (compressed bytes) of traffic is far cheaper than the look-back chain.
+__host__ __device__ inline int enc_wave_cellcap(int sublen) { return ((sublen * kLmax / 32 + 2) + 3) / 4 * 4; }
+__host__ __device__ inline size_t hf_encode_tile_words_dev(int pardeg) { return 2 * (((size_t)pardeg + 63) / 64) + 4; }
+__host__ __device__ inline size_t hf_encode_temp_words_dev(int sublen, int pardeg)
+{  // chunk slots at a worst-case stride, then the per-tile cell totals
+  return (size_t)enc_wave_cellcap(sublen) * (size_t)pardeg + hf_encode_tile_words_dev(pardeg);
+}
 constexpr int kPackWaves = 4;
+// per-tile cell totals (tile = kGatherTile consecutive chunks)
+constexpr int kGatherTile = 64;
+// k_hf_tile_sums' last workgroup scans up to kFusedTiles tile totals in one pass (256 threads)
+constexpr int kScanPer = 8;
+constexpr int kFusedTiles = 256 * kScanPer;
 
 __global__ void __launch_bounds__(64 * kPackWaves) k_hf_pack(HfEncodeArgs a, int cellcap)
 {
@@ -194,29 +206,69 @@ __global__ void __launch_bounds__(64 * kPackWaves) k_hf_pack(HfEncodeArgs a, int
   }
 }
 
-// per-tile cell totals (tile = kGatherTile consecutive chunks), one wave per tile
-constexpr int kGatherTile = 64;
-
-// (and, when total_nbit is set, the archive's bit total: one 64-bit atomic per tile, so the
-// finalize step needs no summing launch of its own)
-// (per-tile bit totals go to tile_bits and k_hf_tile_scan sums them: one atomic per tile on the
-// single total_nbit word queued 2,048 waves at the L2 -- 27 us for config 5's 131,072 chunks)
+// per-tile cell totals, one wave per tile.  With a ticket (kPubTicketWords words zeroed per call)
+// and at most kFusedTiles tiles the last workgroup also does k_hf_tile_scan's work: the exclusive
+// scan of the totals, kScanPer consecutive tiles per thread in one pass (one launch fewer).
+// (Per-tile bit totals, not one atomic per tile on the single total_nbit word: those queued
+// 2,048 waves at the L2 -- 27 us for config 5's 131,072 chunks.)
 __global__ void __launch_bounds__(256) k_hf_tile_sums(const uint32_t* __restrict__ par_nbit, int pardeg,
                                                       uint32_t* __restrict__ tile_sum, uint32_t* __restrict__ tile_bits,
-                                                      int ntiles)
+                                                      int ntiles, uint32_t* ticket, unsigned long long* total_nbit)
 {
-  const int lane = threadIdx.x & 63;
-  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (t >= ntiles) return;
-  uint32_t acc = 0, bits = 0;
-  for (int i = t * kGatherTile + lane; i < min((t + 1) * kGatherTile, pardeg); i += 64) {
-    const uint32_t nb = par_nbit[i];
-    acc += (nb + 31) >> 5;
-    bits += nb;  // a tile of 64 chunks of <= 8192 codes of <= 27 bits: < 2^32
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int t = blockIdx.x * 4 + wid;
+  if (t < ntiles) {
+    uint32_t acc = 0, bits = 0;
+    for (int i = t * kGatherTile + lane; i < min((t + 1) * kGatherTile, pardeg); i += 64) {
+      const uint32_t nb = par_nbit[i];
+      acc += (nb + 31) >> 5;
+      bits += nb;  // a tile of 64 chunks of <= 8192 codes of <= 27 bits: < 2^32
+    }
+    acc = wave_sum(acc);
+    bits = wave_sum(bits);
+    if (lane == 0) {  // (agent scope: the last workgroup may read them from another XCD)
+      __hip_atomic_store(tile_sum + t, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(tile_bits + t, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
-  acc = wave_sum(acc);
-  bits = wave_sum(bits);
-  if (lane == 0) tile_sum[t] = acc, tile_bits[t] = bits;
+  if (!ticket || !last_block(ticket)) return;
+  __shared__ uint32_t s_wc[4];
+  __shared__ unsigned long long s_wb[4];
+  unsigned long long tb = 0;  // this thread's share of the bit total
+  uint32_t carry = 0;
+  for (int base = 0; base < ntiles; base += 256 * kScanPer) {
+    uint32_t v[kScanPer], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; k++) {
+      const int i = base + (int)threadIdx.x * kScanPer + k;
+      v[k] = i < ntiles ? __hip_atomic_load(tile_sum + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      tb += i < ntiles ? __hip_atomic_load(tile_bits + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      sum += v[k];
+    }
+    const uint32_t inc = wave_incl_scan(sum, lane);
+    if (lane == 63) s_wc[wid] = inc;
+    __syncthreads();
+    uint32_t run = carry, tot = carry;
+    for (int w = 0; w < 4; w++) tot += s_wc[w], run += w < wid ? s_wc[w] : 0u;
+    run += inc - sum;
+#pragma unroll
+    for (int k = 0; k < kScanPer; k++) {
+      const int i = base + (int)threadIdx.x * kScanPer + k;
+      if (i < ntiles) tile_sum[i] = run;
+      run += v[k];
+    }
+    carry = tot;
+    __syncthreads();
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) tb += __shfl_xor(tb, d);
+  if (lane == 0) s_wb[wid] = tb;
+  __syncthreads();
+  if (threadIdx.x == 0 && total_nbit) {
+    unsigned long long tot = 0;
+    for (int w = 0; w < 4; w++) tot += s_wb[w];
+    *total_nbit = tot;
+  }
 }
 
 // exclusive scan of the tile totals in place (one workgroup; ntiles <= 1024 * 8)
@@ -884,7 +936,6 @@ __global__ void __launch_bounds__(64 * kDecWaves) k_hf_decode(HfDecodeArgs a, in
 
 }  // namespace
 
-static int enc_wave_cellcap(int sublen) { return ((sublen * kLmax / 32 + 2) + 3) / 4 * 4; }
 
 int hf_encode_groups(int sublen, int pardeg)
 {
@@ -892,11 +943,11 @@ int hf_encode_groups(int sublen, int pardeg)
   return (pardeg + kEncW - 1) / kEncW;
 }
 
-static size_t hf_encode_tile_words(int pardeg) { return 2 * (((size_t)pardeg + kGatherTile - 1) / kGatherTile) + 4; }
-
-size_t hf_encode_temp_words(int sublen, int pardeg)
-{  // chunk slots at a worst-case stride, then the per-tile cell totals
-  return (size_t)enc_wave_cellcap(sublen) * (size_t)pardeg + hf_encode_tile_words(pardeg);
+static_assert(kGatherTile == 64, "hf_encode_tile_words_dev");
+size_t hf_encode_temp_words(int sublen, int pardeg) { return hf_encode_temp_words_dev(sublen, pardeg); }
+static size_t hf_encode_tile_offset(int sublen, int pardeg)
+{
+  return hf_encode_temp_words_dev(sublen, pardeg) - hf_encode_tile_words_dev(pardeg);
 }
 
 // sublen: a multiple of 256 (the pipeline rounds it), so every chunk is a whole number of
@@ -916,10 +967,12 @@ int launch_hf_encode(const HfEncodeArgs& a, hipStream_t st)
   const int grid = need < per_cu * ncu ? need : per_cu * ncu;
   k_hf_pack<<<grid, 64 * kPackWaves, lds, st>>>(a, cellcap);
   const int ntiles = (a.pardeg + kGatherTile - 1) / kGatherTile;
-  uint32_t* tile_sum = a.temp + hf_encode_temp_words(a.sublen, a.pardeg) - hf_encode_tile_words(a.pardeg);
+  uint32_t* tile_sum = a.temp + hf_encode_tile_offset(a.sublen, a.pardeg);
   uint32_t* tile_bits = tile_sum + ntiles;
-  k_hf_tile_sums<<<(ntiles + 3) / 4, 256, 0, st>>>(a.par_nbit, a.pardeg, tile_sum, tile_bits, ntiles);
-  k_hf_tile_scan<<<1, 1024, 0, st>>>(tile_sum, tile_bits, ntiles, a.total_nbit);
+  uint32_t* const ticket = ntiles <= kFusedTiles ? a.ticket : nullptr;
+  k_hf_tile_sums<<<(ntiles + 3) / 4, 256, 0, st>>>(a.par_nbit, a.pardeg, tile_sum, tile_bits, ntiles, ticket,
+                                                   a.total_nbit);
+  if (!ticket) k_hf_tile_scan<<<1, 1024, 0, st>>>(tile_sum, tile_bits, ntiles, a.total_nbit);
   k_hf_gather<<<ntiles, 256, 0, st>>>(a, cellcap, tile_sum);
   return (int)hipGetLastError();
 }

@@ -76,6 +76,8 @@ struct HfEncodeArgs {
   unsigned int* timeout;       // set nonzero if a bounded spin gave up
   uint32_t* temp;              // scratch of hf_encode_temp_words(); nullptr = look-back encoder
   unsigned long long* total_nbit = nullptr;  // if set (zeroed before): the tile-sum pass adds every chunk's bits
+  uint32_t* ticket = nullptr;  // kPubTicketWords words zeroed per call: up to 2,048 tiles the tile-sum
+                               // launch's last workgroup scans them (k_hf_tile_scan not launched)
 };
 int launch_hf_encode(const HfEncodeArgs& a, hipStream_t st);
 size_t hf_encode_temp_words(int sublen, int pardeg);

@@ -659,6 +659,7 @@ struct Pipeline {
                     timeout(),
                     d_enc_temp};
     ea.total_nbit = &info()->total_nbit;  // summed by the encoder's tile-sum pass
+    ea.ticket = plan_ticket();            // (the brick plan's ticket: unused on this path)
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_hf_encode(ea, stream));
     mark(4);
 
