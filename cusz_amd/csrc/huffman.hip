@@ -106,15 +106,13 @@ __device__ __forceinline__ void load_codes16(const uint16_t* p, int mine, uint32
 // latency, not bandwidth, bounds it (measured in round 1).  Here:
 //  (1) k_hf_pack: persistent waves, one chunk per wave at a time, codes prefetched a round
 //      ahead; the chunk's cells go to a scratch slot at a fixed worst-case stride;
-//  (2) k_hf_chunk_scan: one workgroup scans the per-chunk cell counts into par_entry;
-//  (3) k_hf_gather: one wave per chunk copies its cells to their final place (coalesced).
+//  (2) k_hf_tile_sums: cells and bits per tile of 64 chunks; its last workgroup scans the tile
+//      totals into tile offsets (k_hf_tile_scan, a launch of its own, past kFusedTiles tiles);
+//  (3) k_hf_gather: per tile, par_entry from the tile offset + an in-tile scan, then the
+//      chunks' cells copied to their final place (coalesced).
 // The extra 2 x (compressed bytes) of traffic is far cheaper than the look-back chain.
-__host__ __device__ inline int enc_wave_cellcap(int sublen) { return ((sublen * kLmax / 32 + 2) + 3) / 4 * 4; }
-__host__ __device__ inline size_t hf_encode_tile_words_dev(int pardeg) { return 2 * (((size_t)pardeg + 63) / 64) + 4; }
-__host__ __device__ inline size_t hf_encode_temp_words_dev(int sublen, int pardeg)
-{  // chunk slots at a worst-case stride, then the per-tile cell totals
-  return (size_t)enc_wave_cellcap(sublen) * (size_t)pardeg + hf_encode_tile_words_dev(pardeg);
-}
+static int enc_wave_cellcap(int sublen) { return ((sublen * kLmax / 32 + 2) + 3) / 4 * 4; }
+static size_t hf_encode_tile_words(int pardeg) { return 2 * (((size_t)pardeg + 63) / 64) + 4; }
 constexpr int kPackWaves = 4;
 // per-tile cell totals (tile = kGatherTile consecutive chunks)
 constexpr int kGatherTile = 64;
@@ -943,11 +941,14 @@ int hf_encode_groups(int sublen, int pardeg)
   return (pardeg + kEncW - 1) / kEncW;
 }
 
-static_assert(kGatherTile == 64, "hf_encode_tile_words_dev");
-size_t hf_encode_temp_words(int sublen, int pardeg) { return hf_encode_temp_words_dev(sublen, pardeg); }
+static_assert(kGatherTile == 64, "hf_encode_tile_words");
+size_t hf_encode_temp_words(int sublen, int pardeg)
+{  // chunk slots at a worst-case stride, then the per-tile cell and bit totals
+  return (size_t)enc_wave_cellcap(sublen) * (size_t)pardeg + hf_encode_tile_words(pardeg);
+}
 static size_t hf_encode_tile_offset(int sublen, int pardeg)
 {
-  return hf_encode_temp_words_dev(sublen, pardeg) - hf_encode_tile_words_dev(pardeg);
+  return hf_encode_temp_words(sublen, pardeg) - hf_encode_tile_words(pardeg);
 }
 
 // sublen: a multiple of 256 (the pipeline rounds it), so every chunk is a whole number of
