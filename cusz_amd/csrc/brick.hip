@@ -631,19 +631,27 @@ __global__ void __launch_bounds__(kPlanThreads) k_brick_plan(BrickPlanArgs a, He
   __syncthreads();
   const uint32_t nblk = gridDim.x, b0 = blockIdx.x * kPlanBricks;
   unsigned long long wbits = 0;
+  // every histogram of the wave's units is requested before the first is used: bhs <= 1024, two
+  // 16-B loads (8 bins each) per lane and unit, bins past bhs (and units past the end) read 0
+  constexpr int kPer = kPlanBricks / kPlanWaves;
+  const int i0 = lane * 8, i1 = lane * 8 + 512;
+  const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.bhist), 0, (int)min((size_t)a.nunits * a.bhs * 2u, (size_t)0x7FFFFFFF), 0x00020000);
+  u32x4_t hv[kPer][2];
 #pragma unroll
-  for (int j = 0; j < kPlanBricks / kPlanWaves; j++) {
-    const uint32_t slot = wid * (kPlanBricks / kPlanWaves) + j, brick = b0 + slot;
+  for (int j = 0; j < kPer; j++) {
+    const uint32_t brick = b0 + wid * kPer + j;
+    const uint32_t hb = brick * (uint32_t)a.bhs * 2u;
+    hv[j][0] = __builtin_amdgcn_raw_buffer_load_b128(rh, (int)(brick < a.nunits && i0 < a.bhs ? hb + i0 * 2u : 0x80000000u), 0, 0);
+    hv[j][1] = __builtin_amdgcn_raw_buffer_load_b128(rh, (int)(brick < a.nunits && i1 < a.bhs ? hb + i1 * 2u : 0x80000000u), 0, 0);
+  }
+#pragma unroll
+  for (int j = 0; j < kPer; j++) {
+    const uint32_t slot = wid * kPer + j, brick = b0 + slot;
     uint32_t ub = 0, oc = 0;
     if (brick < a.nunits) {
-      const uint16_t* h = a.bhist + (size_t)brick * a.bhs;
       uint32_t bits = 0;
-      // bhs <= 1024: two 16-B loads (8 bins each) per lane
-      const int i0 = lane * 8, i1 = lane * 8 + 512;
-      const uint4 z4 = make_uint4(0, 0, 0, 0);
-      const uint4 v0 = i0 < a.bhs ? *reinterpret_cast<const uint4*>(h + i0) : z4;
-      const uint4 v1 = i1 < a.bhs ? *reinterpret_cast<const uint4*>(h + i1) : z4;
-      const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      const uint32_t w[8] = {hv[j][0].x, hv[j][0].y, hv[j][0].z, hv[j][0].w, hv[j][1].x, hv[j][1].y, hv[j][1].z, hv[j][1].w};
 #pragma unroll
       for (int k = 0; k < 8; k++) {
         const int i = (k < 4 ? i0 : i1) + 2 * (k & 3);
