@@ -597,12 +597,11 @@ __global__ void __launch_bounds__(256) k_x1d_bounds(const uint32_t* __restrict__
                                                     uint32_t nbricks, uint32_t* bstart, uint32_t* unsorted,
                                                     uint32_t epoch, uint32_t ushift)
 {
-  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < ncell; i += (size_t)gridDim.x * 256) {
-    const uint32_t idx = cells[2 * i + 1];
+  // cell i's index against its predecessor's (ip, read only when i > 0)
+  auto cell = [&](size_t i, uint32_t idx, uint32_t ip) {
     const int64_t b = idx < n ? (int64_t)(idx >> ushift) : (int64_t)nbricks;
     int64_t bp = -1;
     if (i > 0) {
-      const uint32_t ip = cells[2 * i - 1];
       if (ip >= idx) *unsorted = epoch;
       bp = ip < n ? (int64_t)(ip >> ushift) : (int64_t)nbricks;
     }
@@ -610,7 +609,25 @@ __global__ void __launch_bounds__(256) k_x1d_bounds(const uint32_t* __restrict__
     for (int64_t u = bp + 1; u <= b && u <= (int64_t)nbricks; u++) bstart[u] = (uint32_t)i;
     if (i + 1 == ncell)
       for (int64_t u = b + 1; u <= (int64_t)nbricks; u++) bstart[u] = (uint32_t)ncell;
+  };
+  // four cells per thread and step (two 16-B loads; the predecessor's index from the cache), up
+  // to 2^28 cells (32-bit buffer offsets); the rest one by one
+  const size_t nq = ncell < (1u << 28) ? ncell / 4 : 0;
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint32_t*>(cells), 0, (int)(nq * 32u), 0x00020000);
+  for (size_t q = blockIdx.x * (size_t)256 + threadIdx.x; q < nq; q += (size_t)gridDim.x * 256) {
+    typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+    const u32x4v v0 = __builtin_amdgcn_raw_buffer_load_b128(rc, (int)(q * 32u), 0, 0);
+    const u32x4v v1 = __builtin_amdgcn_raw_buffer_load_b128(rc, (int)(q * 32u + 16u), 0, 0);
+    const uint32_t ip = q > 0 ? __builtin_amdgcn_raw_buffer_load_b32(rc, (int)(q * 32u - 4u), 0, 0) : 0u;
+    const size_t i = 4 * q;
+    cell(i, v0.y, ip);
+    cell(i + 1, v0.w, v0.y);
+    cell(i + 2, v1.y, v0.w);
+    cell(i + 3, v1.w, v1.y);
   }
+  for (size_t i = 4 * nq + blockIdx.x * (size_t)256 + threadIdx.x; i < ncell; i += (size_t)gridDim.x * 256)
+    cell(i, cells[2 * i + 1], i > 0 ? cells[2 * i - 1] : 0u);
 }
 
 // =========================================================================================
@@ -731,7 +748,7 @@ int launch_x1d_bounds(const uint32_t* cells, size_t ncell, size_t n, uint32_t nb
                       uint32_t* unsorted, uint32_t epoch, hipStream_t st, uint32_t ushift)
 {
   if (ncell == 0) return 0;
-  uint32_t grid = cdiv(ncell, 256);
+  uint32_t grid = cdiv((ncell + 3) / 4, 256);
   if (grid > 4096) grid = 4096;
   k_x1d_bounds<<<grid, 256, 0, st>>>(cells, ncell, n, nbricks, bstart, unsorted, epoch, ushift);
   return (int)hipGetLastError();
