@@ -9,6 +9,7 @@
 
 #include "archive_device.hh"
 #include "common.hh"
+#include "hf_device.hh"
 #include "kernels.hh"
 #include "pub_device.hh"
 
@@ -87,12 +88,7 @@ __global__ void __launch_bounds__(1024) k_finalize_scan(FinalizeArgs a, HeaderTp
     const uint4 v = nxt;
     nxt = load4(base + 256 + 4 * lane);
     const uint32_t own = v.x + v.y + v.z + v.w;
-    uint32_t inc = own;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t t = __shfl_up(inc, d);
-      if (lane >= d) inc += t;
-    }
+    const uint32_t inc = hfd::wave_incl_scan(own);  // DPP: no LDS round trips in the loop
     const uint32_t b = base + 4 * lane;
     uint32_t r = carry + inc - own;
     if (b < w1) a.brick_off[b] = r;
