@@ -24,9 +24,10 @@
 //   decompress (k_brick3_decode): one wave per brick, one chunk per lane decoded in x-blocks of
 //                            64 symbols into an LDS code tile; the block is reconstructed
 //                            (reference scan order) and stored as whole rows.
-// Sampled-codebook mode (k_brick3_sample, k_brick3_single, k_brick3_single_finish): the book
-// comes from every 16th brick before the field is predicted, and one pass predicts, sizes (look-
-// back over the bricks) and packs each brick; see the section before the launchers.
+// Single-pass mode (k_brick3_sample, k_brick3_stream, k_brick3_stream_finish): the book comes
+// from a 1/16 sample of 32 x 8 x 8 units before the field is predicted, and one pass -- a
+// workgroup per brick, a wave per y-step -- predicts, sizes (look-back over the bricks) and packs
+// each brick; see the section before the launchers.
 // The archive is the reference phf format: par_entry[c] points at chunk c (the reference decoder
 // reads chunk c from there, hf_kernels.cuhip.inl:386-391); chunks are laid out brick by brick,
 // and the few cells between a brick's last chunk and the next region are zero.
@@ -34,7 +35,6 @@
 #include <type_traits>
 
 #include "archive_device.hh"
-#include "book_device.hh"
 #include "common.hh"
 #include "hf_device.hh"
 #include "kernels.hh"
@@ -2188,25 +2188,28 @@ k_chunk_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const 
 
 
 // =========================================================================================
-// sampled-codebook mode: sample -> device codebook -> one streaming pass
+// single-pass mode (PSZ_AMD_CODEBOOK_STREAM): sample -> host codebook -> one streaming pass
 // =========================================================================================
 // North-star pins the quant codes, the outliers and the reconstruction, not the bitstream, so
 // the codebook may come from a sample and the field need be read only once:
 //  * k_brick3_sample: the exact codes of a systematic 1/16 sample of 32 x 8 x 8 units (four 8^3
 //    tiles: the units cycle through every x position and visit every (y, z) tile row), one unit
-//    per wave step with all 8 z-rows in flight; its last workgroup builds the canonical codebook
-//    from sample + 1 per bin (every code encodable) on the device (book_device.hh) and writes the
-//    book and the archive's reverse book.  No host round trip.
-//  * k_brick3_stream: persistent waves claim bricks in order from a ticket; a wave predicts its
-//    brick row by row (rows streamed kStreamAhead ahead, across bricks), looks each row's four
-//    codewords per lane up in the LDS book and packs the row at once into its LDS staging buffer
-//    (the packing overlaps the loads in flight), publishes the brick's size, takes its archive
-//    offset by a decoupled look-back over the bricks before it (256 status words per step) and
-//    copies the packed brick out.  A brick that outgrows the staging takes its offset early and
-//    flushes as it goes.  Codes never travel through HBM; no plan pass; no gaps between bricks.
-//  * k_brick3_stream_finish: outlier segment (brick slots in brick order, then the spill list),
-//    totals, both headers; the last workgroup publishes the compress summary.
-// Deadlock-free: a look-back only waits on bricks claimed earlier, whose waves are running.
+//    per wave step with all 8 z-rows in flight; its last workgroup hands the histogram to the
+//    host (host-mapped), which builds the two-queue book of sample + 1 (every code encodable).
+//  * k_brick3_stream: ONE WORKGROUP PER BRICK, wave y owning the brick's y-step y (rows (y, z),
+//    z = 0..7): the wave predicts its 8 rows (z-diff and the x-diff inside the 8-wide tiles in
+//    registers; the y-diff against wave y - 1's z/x residuals, exchanged through LDS), looks the
+//    codewords up and sums each row's bits.  The workgroup's total is the brick's size: wave 0
+//    publishes it for the decoupled look-back over the bricks before it while every wave packs
+//    its rows into its own LDS area, and once the offset is known each wave writes its rows
+//    straight to the archive.  Codes never touch HBM, nothing is staged per brick beyond a
+//    y-step's cells, there is no plan pass and no gap between bricks.  Workgroup 0 takes the
+//    host's book (a device-polled gate) while every workgroup predicts its first brick.
+//  * k_brick3_stream_finish: outlier segment (the per-(brick, y-step) slots in brick order, then
+//    the spill list), totals, both headers; the last workgroup publishes the compress summary.
+// Deadlock-free: bricks are claimed in ticket order by resident workgroups, a workgroup claims
+// its next brick only while working on an earlier one, and a look-back waits only on aggregates
+// of smaller tickets -- the smallest unfinished brick always has every predecessor's.
 constexpr uint32_t kSampleStride = 16;
 constexpr unsigned long long kStAgg = 1ull << 62, kStInc = 2ull << 62;  // look-back status flags
 
@@ -2229,14 +2232,14 @@ __device__ __forceinline__ T shfl_up8(T v)
   }
 }
 
-constexpr int kSampleThreads = hbook::kThreads;  // the last workgroup builds the book
+constexpr int kSampleThreads = 256;
 template <typename T, bool ZZ>
 __global__ void __launch_bounds__(kSampleThreads)
 k_brick3_sample(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T ebx2_r, T r,
-                uint32_t* __restrict__ g_hist, int bklen, uint32_t* ticket, uint32_t* book, uint8_t* revbook)
+                uint32_t* __restrict__ g_hist, int bklen, uint32_t* ticket, uint32_t* h_hist, uint32_t* flag,
+                uint32_t epoch)
 {
   __shared__ uint32_t s_h[kMaxBklen];
-  __shared__ hbook::Smem s_book;
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   for (int i = threadIdx.x; i < bklen; i += blockDim.x) s_h[i] = 0;
   __syncthreads();
@@ -2288,63 +2291,17 @@ k_brick3_sample(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz,
       }
     }
   }
+  // bins one 64-B line apart (kSampleBinStride): the workgroups finish together, and their
+  // atomics would queue on the few lines of a dense array
   __syncthreads();
   for (int i = threadIdx.x; i < bklen; i += blockDim.x)
-    if (s_h[i]) atomicAdd(&g_hist[i], s_h[i]);
-  if (!last_block(ticket)) return;
+    if (s_h[i]) atomicAdd(&g_hist[i * kSampleBinStride], s_h[i]);
+  if (!last_block(ticket)) return;  // the last workgroup: the sample histogram -> the host, flag raised
   for (int i = threadIdx.x; i < bklen; i += blockDim.x)
-    s_h[i] = __hip_atomic_load(g_hist + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    h_hist[i] = __hip_atomic_load(g_hist + i * kSampleBinStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __threadfence_system();
   __syncthreads();
-  hbook::build<kSampleThreads>(s_h, bklen, 1u, book, revbook, s_book);
-}
-
-// 1-D: sample units are the reference's 1024-element tiles (lrz_c.cuhip.inl:23-109), every 16th
-// from 4096 tiles up (u = 16 i + i % 16), else every tile; lane l predicts elements [16 l, 16 l + 16)
-// of the tile (the element before a lane's first from lane l - 1, 0 at the tile start)
-__host__ __device__ inline uint32_t sample_units1(size_t n) { return (uint32_t)((n + 1023) / 1024); }
-
-template <typename T, bool ZZ>
-__global__ void __launch_bounds__(kSampleThreads)
-k_brick1_sample(const T* __restrict__ in, size_t n, T ebx2_r, T r, uint32_t* __restrict__ g_hist, int bklen,
-                uint32_t* ticket, uint32_t* book, uint8_t* revbook)
-{
-  __shared__ uint32_t s_h[kMaxBklen];
-  __shared__ hbook::Smem s_book;
-  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  for (int i = threadIdx.x; i < bklen; i += blockDim.x) s_h[i] = 0;
-  __syncthreads();
-  const uint32_t units = sample_units1(n), stride = sample_stride(units), nsamp = (units + stride - 1) / stride;
-  constexpr int kW = kSampleThreads / 64;
-  for (uint32_t i = blockIdx.x * kW + wid; i < nsamp; i += gridDim.x * kW) {
-    const uint32_t u = i * stride + i % stride;
-    if (u >= units) continue;  // (uniform)
-    const size_t e0 = (size_t)u * 1024 + (size_t)lane * 16;
-    T v[16];
-#pragma unroll
-    for (int g = 0; g < 4; g++) load_row<T, 4>(in, e0, 4 * g, (uint32_t)min<size_t>(16, n > e0 ? n - e0 : 0), true,
-                                             reinterpret_cast<T(&)[4]>(v[4 * g]));
-    T p[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) p[k] = dround(v[k] * ebx2_r);
-    T west = __shfl_up(p[15], 1);
-    if (lane == 0) west = (T)0;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-      const T d = p[k] - (k ? p[k - 1] : west);
-      bool ol;
-      float ov;
-      const uint16_t c = quantize<T, ZZ>(d, r, ol, ov);
-      if (e0 + k < n) atomicAdd(&s_h[c], 1u);
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < bklen; i += blockDim.x)
-    if (s_h[i]) atomicAdd(&g_hist[i], s_h[i]);
-  if (!last_block(ticket)) return;
-  for (int i = threadIdx.x; i < bklen; i += blockDim.x)
-    s_h[i] = __hip_atomic_load(g_hist + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  hbook::build<kSampleThreads>(s_h, bklen, 1u, book, revbook, s_book);
+  if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __device__ __forceinline__ unsigned long long st_word(unsigned long long flag, uint32_t cells, uint32_t oc)
@@ -2395,8 +2352,8 @@ __device__ __forceinline__ void lookback(const unsigned long long* status, uint3
 
 struct StreamArgs {
   uint32_t lx, ly, lz, nbx, nby, nbricks;
-  OutlierSink ol;
-  const uint32_t* book;
+  OutlierSink ol;              // one slot per (brick, y-step): slot 8 brick + y, cap_per_brick = its cap
+  uint32_t* book;              // device book: written by workgroup 0 from the host's
   int bklen;
   uint32_t* par_nbit;
   uint32_t* par_entry;
@@ -2404,218 +2361,375 @@ struct StreamArgs {
   uint32_t bs_cap;             // bitstream capacity (cells)
   unsigned long long* status;  // per brick, zeroed per call
   uint32_t* ticket;            // zeroed per call
-  uint32_t* ol_pre;            // per brick: exclusive prefix of slot outliers
+  uint32_t* ol_dst;            // per slot: its first cell in the archive's outlier segment
   CompressInfo* info;
   unsigned int* timeout;
+  // the codebook gate: the host writes the book and reverse book to host-mapped memory and sets
+  // *gate = gate_epoch; workgroup 0 copies them to `book` and the archive, then sets *book_flag
+  const uint32_t* gate;
+  uint32_t gate_epoch;
+  const uint32_t* h_book;
+  const uint32_t* h_revbook;
+  uint32_t* revbook;  // the archive's reverse book
+  int rv_words;
+  uint32_t* book_flag;  // device word, never reset (epoch-compared)
 };
 
-constexpr int kStreamWaves = 4;
-constexpr int kStageWords = 4608;  // per-wave staging of the packed brick (18 KB: 8 waves per CU)
-static_assert(kStageWords >= 2 * kPackRowMax, "a brick row always fits");
+constexpr int kStreamWaves = 8;  // one wave per y-step of the brick
+#ifndef CUSZ_AMD_STREAM_PF_LATE
+#define CUSZ_AMD_STREAM_PF_LATE 0  // 1: the next brick's rows are issued after barrier B, not A
+#endif
+// LDS per workgroup: waves 0..6 hand their y-step's z/x residuals to the next wave (the y-diff)
+// through an exchange area; every wave stages its y-step's packed cells in a staging area until
+// the brick's offset is known (one brick later: the look-back is deferred)
 template <typename T>
-constexpr int kStreamAhead = 8;  // rows in flight per wave
+constexpr int kStreamXsWords = 8 * 64 * 4 * (int)sizeof(T) / 4;
+constexpr int kStageW = 512;  // staging words per wave
+static_assert(kStageW >= 2 * kPackRowMax + 2, "the flush path holds two rows");
+template <typename T>
+constexpr size_t stream_lds_bytes()
+{
+  return ((size_t)(kStreamWaves - 1) * kStreamXsWords<T> + (size_t)kStreamWaves * kStageW) * 4;
+}
+constexpr uint32_t kNoBrick = 0xFFFFFFFFu;
 
+// Single-pass encoder, one workgroup per brick, wave y = the brick's y-step y.  Per brick:
+//   phase 1   prequant, z-diff, x-diff of the wave's 8 rows (loaded one brick ahead), residuals
+//             -> the exchange area; (A) the next brick's rows are issued, y-diff from the area
+//   phase 2   codes, outliers (the y-step's slot), row bits (LDS book), row scans; (B) sizes
+//   wave 0    publishes the brick's aggregate, then looks back for the PREVIOUS brick (its
+//             predecessors published a brick ago: the walk rarely waits) and publishes its
+//             inclusive prefix; (C)
+//   all       copy the previous brick's staged cells out, then pack this brick's into staging.
+// A brick with a y-step too large for the staging (noisy fields) takes its own offset at once
+// and packs through the staging area with flushes.
 template <typename T, bool ZZ>
-__global__ void __launch_bounds__(64 * kStreamWaves) __attribute__((amdgpu_waves_per_eu(1, 2)))  // LDS: 2 per SIMD
+__global__ void __launch_bounds__(64 * kStreamWaves)
+__attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? 4 : 2)))  // f32: 2 workgroups per CU (LDS, 128 VGPRs)
 k_brick3_stream(const T* __restrict__ in, StreamArgs a, T ebx2_r, T r)
 {
   constexpr int V = 4;
+  constexpr int XW = kStreamXsWords<T>;
+  extern __shared__ uint32_t smem[];  // exchange areas (waves 0..6), then staging areas
   __shared__ uint32_t s_book[kMaxBklen];
-  __shared__ uint32_t s_stage[kStreamWaves][kStageWords + 4];  // + pack4_or_lj's zero slack
+  __shared__ uint32_t s_wc[kStreamWaves], s_wo[kStreamWaves];
+  __shared__ uint32_t s_next[2], s_x[4];
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint32_t* const stage = s_stage[wid];
-  for (int i = threadIdx.x; i < a.bklen; i += blockDim.x) s_book[i] = a.book[i];
-  for (int i = lane; i < kStageWords + 4; i += 64) stage[i] = 0;
-  __syncthreads();
+  T* const xsT = reinterpret_cast<T*>(smem + (wid < kStreamWaves - 1 ? wid : 0) * XW);
+  const T* const xprev = reinterpret_cast<const T*>(smem + (wid > 0 ? wid - 1 : 0) * XW);
+  uint32_t* const stg = smem + (kStreamWaves - 1) * XW + wid * kStageW;
   const StepLoader<T, V> ld{in, (size_t)a.lx * a.ly, a.lx, a.ly, a.lz, a.nbx, a.nby, a.nbricks, 0, (uint32_t)lane};
-  const size_t plane = ld.plane;
-  auto claim = [&]() -> uint32_t {
-    uint32_t b = 0;
-    if (lane == 0) b = atomicAdd(a.ticket, 1u);
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
-  };
-  uint32_t brick = claim();
-  // one y-step (the 8 z-rows of one y) in flight: loaded while the previous one is computed
-  T q[8][V];
+  const uint32_t subcap = a.ol.cap_per_brick;
+
+  // workgroup 0, wave 0: the host's codebook -> device memory and the archive, then the flag
+  if (blockIdx.x == 0 && wid == 0) {
+    uint32_t ok = 1;
+    if (lane == 0) {
+      for (uint32_t spin = 0;; spin++) {
+        const uint32_t v = __hip_atomic_load(a.gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((int32_t)(v - a.gate_epoch) >= 0) break;
+        if (spin > (1u << 22)) {
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    ok = (uint32_t)__builtin_amdgcn_readfirstlane((int)ok);
+    if (!ok && lane == 0) atomicOr(a.timeout, 2u);
+    for (int i = lane; i < a.bklen; i += 64) a.book[i] = a.h_book[i];
+    for (int i = lane; i < a.rv_words; i += 64) a.revbook[i] = a.h_revbook[i];
+    __builtin_amdgcn_s_waitcnt(0);
+    hfd::wave_sync();
+    if (lane == 0) __hip_atomic_store(a.book_flag, a.gate_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+
+  if (threadIdx.x == 0) s_next[0] = atomicAdd(a.ticket, 1u);
+  __syncthreads();
+  uint32_t brick = s_next[0];
+  T q[8][V];  // this wave's rows of the brick (loaded one brick ahead)
 #pragma unroll
-  for (int z = 0; z < 8; z++) ld.issue_row(brick, z, q[z]);
-  while (brick < a.nbricks) {
-    const uint32_t bnext = claim();
+  for (int z = 0; z < 8; z++) ld.issue_row(brick, 8 * wid + z, q[z]);
+  bool have_book = false;
+  unsigned long long wbits = 0;  // bits this wave packed (the header's total)
+  uint32_t par = 0;
+  // the deferred brick (uniform): its index, totals, this wave's cells / slot outliers before it
+  // and its own; lane z: its row z's bits and first cell
+  uint32_t dbrick = kNoBrick, d_ct = 0, d_ot = 0, d_cb = 0, d_ob = 0, d_cells = 0, d_cnt = 0;
+  uint32_t d_nbit = 0, d_loc = 0;
+  // diagnostic build: per-phase clocks summed over waves (0 wave-bricks, 1 phase 1 incl. the
+  // loads' wait, 2 barrier A + y-diff + book, 3 phase 2, 4 barrier B, 5 look-back (wave 0),
+  // 6 barrier C, 7 copy-out of the deferred brick, 8 pack)
+  BPROF(unsigned long long pc[16] = {}; unsigned long long tk = 0, tp = __builtin_readcyclecounter();)
+#define SPROF(i) BPROF(hfd::wave_sync(); tk = __builtin_readcyclecounter(); pc[i] += tk - tp; tp = tk;)
+  for (;;) {
+    const bool live = brick < a.nbricks;  // (uniform over the workgroup)
+    if (!live && dbrick == kNoBrick) break;
+    BPROF(pc[0] += live;)
     const uint32_t bx = brick % a.nbx, t = brick / a.nbx, by = t % a.nby, bz = t / a.nby;
-    const uint32_t x0 = bx * (64 * V) + lane * V, y0 = by * 8, z0 = bz * 8;
-    const uint32_t nyv = min(8u, a.ly - y0), nzv = min(8u, a.lz - z0);
-    uint32_t cnt = 0;             // outliers of the brick
-    uint32_t off = 0, fbase = 0;  // brick words packed; words [fbase, off) are in the staging
-    uint32_t xc = 0, xo = 0;      // the brick's archive offsets (known early when it flushes)
-    bool direct = false;          // (uniform) offsets taken early: flushes go straight out
-    unsigned long long bbits = 0;
-    uint32_t my_nbit = 0, my_loc = 0;  // lane = row: its bits and first word in the brick
-    // staged words -> the archive (each lane one word per store: the offset has any alignment)
-    auto flush = [&]() {
-      hfd::wave_sync();
-      const uint32_t m = off - fbase;
-      const bool fits = xc + off <= a.bs_cap;
-      if (!fits && lane == 0) atomicOr(a.timeout, 4u);
-      for (uint32_t i = (uint32_t)lane; i < m; i += 64) {
-        const uint32_t v = stage[i];
-        stage[i] = 0;
-        if (fits) a.bitstream[xc + fbase + i] = v;
-      }
-      fbase = off;
-      hfd::wave_sync();
-    };
-    T bprev[8][V];  // the previous y-step's z/x residuals (y-diff)
-#pragma unroll
-    for (int z = 0; z < 8; z++)
-#pragma unroll
-      for (int k = 0; k < V; k++) bprev[z][k] = (T)0;
-#pragma unroll 1
-    for (uint32_t y = 0; y < 8; y++) {
-      // phase 1, straight-line over the y-step's 8 rows: prequant, residuals in the reference
-      // order (z, x inside the 8-wide tile, y), codes; the next y-step's rows are issued as these
-      // are consumed.  Rows outside the field (partial bricks) get no codewords by selects.
-      const bool yok = y0 + y < a.ly;  // (uniform)
-      T d[8][V];
-      uint32_t qc2[8][2];  // the row's 4 codes as two u16 pairs
-      uint64_t anyol = 0;
-      T pprev[V];
-#pragma unroll
-      for (int z = 0; z < 8; z++) {
-        T p[V];
-#pragma unroll
-        for (int k = 0; k < V; k++) p[k] = dround(q[z][k] * ebx2_r);
-        if (y + 1 < 8) ld.issue_row(brick, (int)(8 * (y + 1)) + z, q[z]);
-        else ld.issue_row(bnext, z, q[z]);
-        T av[V];
-#pragma unroll
-        for (int k = 0; k < V; k++) {
-          av[k] = z > 0 ? p[k] - pprev[k] : p[k];
-          pprev[k] = p[k];
-        }
-        const T west = shr_in_tile<T, 1, 8 / V>(av[V - 1]);
-#pragma unroll
-        for (int k = V - 1; k > 0; k--) av[k] = av[k] - av[k - 1];
-        if (x0 % 8 != 0) av[0] = av[0] - west;
-        const bool rok = yok && (uint32_t)z < nzv;
-        uint16_t c[V];
-#pragma unroll
-        for (int k = 0; k < V; k++) {
-          d[z][k] = av[k] - bprev[z][k];
-          bprev[z][k] = av[k];
-          bool is_ol;
-          float ov;
-          c[k] = quantize<T, ZZ>(d[z][k], r, is_ol, ov);
-          anyol |= __ballot(is_ol && rok);
-        }
-        qc2[z][0] = (uint32_t)c[0] | (uint32_t)c[1] << 16;
-        qc2[z][1] = (uint32_t)c[2] | (uint32_t)c[3] << 16;
-      }
-      if (!yok) continue;  // (uniform: the whole y-step lies past the field)
-      // outliers of the y-step into the brick's slot (rare)
-      if (anyol) {
+    const uint32_t x0 = bx * (64 * V) + lane * V, z0 = bz * 8, gy = by * 8 + (uint32_t)wid;
+    const bool yok = live && gy < a.ly;  // (uniform per wave)
+    const uint32_t nzv = live ? min(8u, a.lz - z0) : 0u;
+    const uint32_t slot = brick * kStreamWaves + (uint32_t)wid;
+    uint32_t cnt = 0, cells = 0;
+    uint32_t cp[8][2], inc[8];  // codes as u16 pairs, row scans of the bits (lane 63: the row's bits)
+    bool wide = false;                  // a lane's four codewords of some row exceed 64 bits
+    uint32_t bnext = kNoBrick;
+    if (live) {
+      // phase 1: prequant, z-diff, x-diff inside the 8-wide tile (lrz_c.cuhip.inl:341-352 order)
+      T av[8][V];
+      {
+        T pprev[V];
 #pragma unroll
         for (int z = 0; z < 8; z++) {
-          if ((uint32_t)z >= nzv) break;
-          uint32_t mask = 0;
-          float olv[V];
-          size_t idx[V];
-          const size_t base = (size_t)(z0 + z) * plane + (size_t)(y0 + y) * a.lx;
 #pragma unroll
           for (int k = 0; k < V; k++) {
-            bool is_ol;
-            const uint16_t c = quantize<T, ZZ>(d[z][k], r, is_ol, olv[k]);
-            mask |= (uint32_t)(c == 0 && is_ol) << k;
-            idx[k] = base + x0 + k;
+            const T p = dround(q[z][k] * ebx2_r);
+            av[z][k] = z > 0 ? p - pprev[k] : p;
+            pprev[k] = p;
           }
-          if (__builtin_amdgcn_ballot_w64(mask != 0)) emit_outliers<V>(a.ol, brick, cnt, mask, olv, idx);
+          const T west = shr_in_tile<T, 1, 8 / V>(av[z][V - 1]);
+#pragma unroll
+          for (int k = V - 1; k > 0; k--) av[z][k] = av[z][k] - av[z][k - 1];
+          if (x0 % 8 != 0) av[z][0] = av[z][0] - west;
         }
       }
-      // phase 2: codewords (LDS book), row bits by DPP scans, the y-step's size; the staging
-      // takes the offsets early and flushes when the y-step might not fit (rare)
-      uint32_t w[8][V], bits[8], inc[8], tot[8], cells = 0;
+      if (wid < kStreamWaves - 1)
 #pragma unroll
-      for (int z = 0; z < 8; z++) {
-        const bool rok = (uint32_t)z < nzv;
-        w[z][0] = s_book[qc2[z][0] & 0xFFFFu], w[z][1] = s_book[qc2[z][0] >> 16];
-        w[z][2] = s_book[qc2[z][1] & 0xFFFFu], w[z][3] = s_book[qc2[z][1] >> 16];
-        if (!rok) w[z][0] = w[z][1] = w[z][2] = w[z][3] = 0u;
-        bits[z] = (w[z][0] >> 27) + (w[z][1] >> 27) + (w[z][2] >> 27) + (w[z][3] >> 27);
-        inc[z] = hfd::wave_incl_scan(bits[z]);
-        tot[z] = readlane(inc[z], 63);
-        cells += (tot[z] + 31) >> 5;
-      }
-      if (off - fbase + cells + 2 > (uint32_t)kStageWords) {  // the staging is full: offsets now, flush
-        if (!direct) {
-          lookback(a.status, brick, lane, xc, xo, a.timeout);
-          direct = true;
+        for (int z = 0; z < 8; z++) lds_store4(xsT + ((size_t)z * 64 + lane) * V, av[z]);
+      if (threadIdx.x == 0) s_next[par ^ 1] = atomicAdd(a.ticket, 1u);
+      SPROF(1)
+      __syncthreads();  // (A) residuals exchanged, next brick known
+      bnext = s_next[par ^ 1];
+      par ^= 1;
+#if !CUSZ_AMD_STREAM_PF_LATE
+#pragma unroll
+      for (int z = 0; z < 8; z++) ld.issue_row(bnext, 8 * wid + z, q[z]);
+#endif
+      if (!have_book) {  // first brick: the codebook (workgroup 0 raises the flag)
+        if (threadIdx.x == 0) {
+          for (uint32_t spin = 0;; spin++) {
+            const uint32_t v = __hip_atomic_load(a.book_flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            if (v == a.gate_epoch) break;
+            if (spin > (1u << 22)) {
+              atomicOr(a.timeout, 2u);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
         }
-        flush();
+        __syncthreads();
+        for (int i = threadIdx.x; i < a.bklen; i += 64 * kStreamWaves)
+          s_book[i] = __hip_atomic_load(a.book + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        have_book = true;
       }
-      const bool wide = __builtin_amdgcn_ballot_w64(bits[0] > 64u || bits[1] > 64u || bits[2] > 64u || bits[3] > 64u ||
-                                                    bits[4] > 64u || bits[5] > 64u || bits[6] > 64u || bits[7] > 64u) != 0;
+      SPROF(2)
+      // phase 2: y-diff against the previous y-step (the brick's first y-step has none), codes
+      // (kept as u16 pairs), outliers (into this y-step's slot), row bits
 #pragma unroll
       for (int z = 0; z < 8; z++) {
-        const uint32_t pos = ((off - fbase) << 5) + inc[z] - bits[z];
-        if (!wide)
-          hfd::pack4_or_lj(stage, pos, w[z], bits[z]);
-        else
-          hfd::pack_words<V>(stage, pos, w[z], V);
-        if ((uint32_t)lane == 8 * y + (uint32_t)z) my_nbit = tot[z], my_loc = off;
-        off += (tot[z] + 31) >> 5;
-        bbits += tot[z];
+        const bool rok = yok && (uint32_t)z < nzv;
+        if (wid > 0) {
+          T bp[V];
+          lds_load4(xprev + ((size_t)z * 64 + lane) * V, bp);
+#pragma unroll
+          for (int k = 0; k < V; k++) av[z][k] = av[z][k] - bp[k];
+        }
+        uint16_t c[V];
+        float olv[V];
+        uint32_t mask = 0;
+#pragma unroll
+        for (int k = 0; k < V; k++) {
+          bool is_ol;
+          c[k] = quantize<T, ZZ>(av[z][k], r, is_ol, olv[k]);
+          mask |= (uint32_t)(is_ol && rok) << k;
+        }
+        if (__builtin_amdgcn_ballot_w64(mask != 0)) {  // (rare; the field has < 2^32 elements)
+          const uint32_t base = (uint32_t)((z0 + z) * ld.plane + (size_t)gy * a.lx) + x0;
+          emit_outliers32<V>(a.ol, slot, cnt, mask, olv, base);
+        }
+        uint32_t bits = 0;  // (rows outside the field: no codewords)
+#pragma unroll
+        for (int k = 0; k < V; k++) bits += rok ? s_book[c[k]] >> 27 : 0u;
+        cp[z][0] = (uint32_t)c[0] | (uint32_t)c[1] << 16;
+        cp[z][1] = (uint32_t)c[2] | (uint32_t)c[3] << 16;
+        wide |= bits > 64u;
+        inc[z] = hfd::wave_incl_scan(bits);
+        cells += (readlane(inc[z], 63) + 31) >> 5;
+      }
+      if (lane == 0) s_wc[wid] = cells, s_wo[wid] = min(cnt, subcap);
+      SPROF(3)
+    }
+    __syncthreads();  // (B) every y-step's size; the exchange areas are free
+#if CUSZ_AMD_STREAM_PF_LATE
+    if (live)
+#pragma unroll
+      for (int z = 0; z < 8; z++) ld.issue_row(bnext, 8 * wid + z, q[z]);
+#endif
+    SPROF(4)
+    uint32_t cb = 0, ob = 0, ct = 0, ot = 0, cmax = 0;  // before this wave, brick totals, largest y-step
+    if (live) {
+#pragma unroll
+      for (int v = 0; v < kStreamWaves; v++) {
+        const uint32_t c = s_wc[v], o = s_wo[v];
+        if (v < wid) cb += c, ob += o;
+        ct += c, ot += o;
+        cmax = max(cmax, c);
       }
     }
-    // the brick's place in the archive
-    const uint32_t oc = min(cnt, a.ol.cap_per_brick);
-    if (!direct) {
-      if (brick == 0) {
-        if (lane == 0) __hip_atomic_store(a.status, st_word(kStInc, off, oc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool direct = live && cmax + 2 > (uint32_t)kStageW;  // (uniform) too large to stage: offsets now
+    if (wid == 0) {
+      if (live && lane == 0)  // the brick's aggregate (brick 0: its inclusive prefix)
+        __hip_atomic_store(a.status + brick, st_word(brick == 0 ? kStInc : kStAgg, ct, ot), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      if (dbrick != kNoBrick) {  // the deferred brick's offsets
+        uint32_t xc = 0, xo = 0;
+        if (dbrick != 0) {
+          lookback(a.status, dbrick, lane, xc, xo, a.timeout);
+          if (lane == 0)
+            __hip_atomic_store(a.status + dbrick, st_word(kStInc, xc + d_ct, xo + d_ot), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) s_x[0] = xc, s_x[1] = xo;
+      }
+      if (direct) {  // this brick's offsets at once
+        uint32_t xc = 0, xo = 0;
+        if (brick != 0) {
+          lookback(a.status, brick, lane, xc, xo, a.timeout);
+          if (lane == 0)
+            __hip_atomic_store(a.status + brick, st_word(kStInc, xc + ct, xo + ot), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) s_x[2] = xc, s_x[3] = xo;
+      }
+    }
+    SPROF(5)
+    __syncthreads();  // (C) the offsets
+    SPROF(6)
+    // cells -> the archive, with the brick's chunk tables and slot destination
+    auto emit = [&](uint32_t b, uint32_t woff, uint32_t oo, uint32_t ncells, uint32_t nbit, uint32_t loc,
+                    uint32_t scnt) {
+      const uint32_t bxx = b % a.nbx, tt = b / a.nbx, byy = tt % a.nby, bzz = tt / a.nby;
+      const uint32_t gyy = byy * 8 + (uint32_t)wid, nz = min(8u, a.lz - bzz * 8);
+      if (woff + ncells <= a.bs_cap) {
+        for (uint32_t i = (uint32_t)lane; i < ncells; i += 64) a.bitstream[woff + i] = stg[i];
+      }
+      else if (lane == 0)
+        atomicOr(a.timeout, 4u);
+      if (lane < 8 && gyy < a.ly && (uint32_t)lane < nz) {
+        const size_t c = ((size_t)(bzz * 8 + (uint32_t)lane) * a.ly + gyy) * a.nbx + bxx;
+        a.par_nbit[c] = nbit;
+        a.par_entry[c] = woff + loc;
+      }
+      if (lane == 0) {
+        const uint32_t s = b * kStreamWaves + (uint32_t)wid;
+        a.ol.brick_cnt[s] = scnt;
+        a.ol_dst[s] = oo;
+        if (scnt > subcap) atomicMax(&a.info->max_brick_cnt, scnt * kStreamWaves);  // slot growth
+      }
+    };
+    if (dbrick != kNoBrick) {
+      hfd::wave_sync();
+      emit(dbrick, s_x[0] + d_cb, s_x[1] + d_ob, d_cells, d_nbit, d_loc, d_cnt);
+      dbrick = kNoBrick;
+    }
+    SPROF(7)
+    if (live) {
+      // pack the y-step's rows into the staging area (zeroed first; two words of slack); the
+      // codewords are looked up again (fewer registers live across the barriers than holding them)
+      const bool any_wide = __builtin_amdgcn_ballot_w64(wide) != 0;
+      uint32_t off = 0, fbase = 0, my_nbit = 0, my_loc = 0;  // lane z: row z's bits and first cell
+      const uint32_t woff = direct ? s_x[2] + cb : 0u;
+      auto flush = [&]() {  // (direct) staged words [fbase, off) -> the archive, staging cleared
+        hfd::wave_sync();
+        const uint32_t m = off - fbase;
+        const bool fits = woff + off <= a.bs_cap;
+        if (!fits && lane == 0) atomicOr(a.timeout, 4u);
+        for (uint32_t i = (uint32_t)lane; i < m; i += 64) {
+          const uint32_t v = stg[i];
+          stg[i] = 0u;
+          if (fits) a.bitstream[woff + fbase + i] = v;
+        }
+        fbase = off;
+        hfd::wave_sync();
+      };
+      for (uint32_t i = (uint32_t)lane; i < (direct ? (uint32_t)kStageW : cells + 2); i += 64) stg[i] = 0u;
+#pragma unroll
+      for (int z = 0; z < 8; z++) {
+        if (direct && off - fbase + kPackRowMax > (uint32_t)kStageW) flush();
+        uint32_t w[V];
+        w[0] = s_book[cp[z][0] & 0xFFFFu], w[1] = s_book[cp[z][0] >> 16];
+        w[2] = s_book[cp[z][1] & 0xFFFFu], w[3] = s_book[cp[z][1] >> 16];
+        if (!(yok && (uint32_t)z < nzv)) w[0] = w[1] = w[2] = w[3] = 0u;  // a row outside the field (uniform)
+        const uint32_t bits = (w[0] >> 27) + (w[1] >> 27) + (w[2] >> 27) + (w[3] >> 27);
+        const uint32_t pos = ((off - fbase) << 5) + inc[z] - bits;
+        if (!any_wide)
+          hfd::pack4_or_lj(stg, pos, w, bits);
+        else
+          hfd::pack_words<V>(stg, pos, w, V);
+        const uint32_t tot = readlane(inc[z], 63);
+        if (lane == z) my_nbit = tot, my_loc = off;
+        off += (tot + 31) >> 5;
+        wbits += tot;
+      }
+      if (direct) {
+        flush();
+        emit(brick, woff, s_x[3] + ob, 0u, my_nbit, my_loc, cnt);  // (the cells are out)
       }
       else {
-        if (lane == 0) __hip_atomic_store(a.status + brick, st_word(kStAgg, off, oc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        lookback(a.status, brick, lane, xc, xo, a.timeout);
+        dbrick = brick, d_ct = ct, d_ot = ot, d_cb = cb, d_ob = ob, d_cells = cells, d_cnt = cnt;
+        d_nbit = my_nbit, d_loc = my_loc;
       }
+      brick = bnext;
     }
-    if (lane == 0 && (direct || brick != 0))
-      __hip_atomic_store(a.status + brick, st_word(kStInc, xc + off, xo + oc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flush();
-    const uint32_t ry = lane >> 3, rz = lane & 7;
-    if (ry < nyv && rz < nzv) {
-      const size_t c = ((size_t)(z0 + rz) * a.ly + (y0 + ry)) * a.nbx + bx;
-      a.par_nbit[c] = my_nbit;
-      a.par_entry[c] = xc + my_loc;
-    }
-    if (lane == 0) {
-      a.ol.brick_cnt[brick] = cnt;
-      if (cnt > a.ol.cap_per_brick) atomicMax(&a.info->max_brick_cnt, cnt);  // slot growth
-      a.ol_pre[brick] = xo;
-      atomicAdd(&a.info->total_nbit, bbits);
-    }
-    brick = bnext;
+    SPROF(8)
   }
+#undef SPROF
+  if (lane == 0 && wbits) atomicAdd(&a.info->total_nbit, wbits);
+#ifdef CUSZ_AMD_DEC_PROFILE
+  if (lane == 0)
+    for (int i = 0; i < 16; i++) atomicAdd(&g_brick_prof[i], pc[i]);
+#endif
 }
 
-// after the streaming pass: the outlier segment (slots in brick order, then the spill list), the
-// totals and both headers; the last workgroup publishes the compress summary
-__global__ void __launch_bounds__(256) k_brick3_stream_finish(StreamArgs a, HeaderTpl tpl, uint8_t* archive,
-                                                              size_t phf_offset, size_t bits_rel, HostPub pub)
+// after the streaming pass: the outlier segment (the slots in (brick, y-step) order -- brick
+// order, row order inside a brick -- then the spill list), the totals and both headers; the last
+// workgroup publishes the compress summary.  Each wave copies 64 consecutive slots: their
+// destinations are one contiguous range, a cell finds its slot by a binary search over the
+// slots' prefix counts.
+constexpr int kFinishThreads = 256;
+__global__ void __launch_bounds__(kFinishThreads) k_brick3_stream_finish(StreamArgs a, HeaderTpl tpl, uint8_t* archive,
+                                                                         size_t phf_offset, size_t bits_rel, HostPub pub)
 {
+  __shared__ uint32_t s_ex[kFinishThreads / 64][65];
   const unsigned long long last =
       __hip_atomic_load(a.status + a.nbricks - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t ncell = (uint32_t)last, slot_total = (uint32_t)(last >> 32) & 0x3FFFFFFFu;
   uint2* ol_dst = reinterpret_cast<uint2*>(a.bitstream + ncell);
-  const uint32_t lane = threadIdx.x & 63, nwv = gridDim.x * 4;
-  for (uint32_t b = (blockIdx.x * 256 + threadIdx.x) >> 6; b < a.nbricks; b += nwv) {
-    const uint32_t cnt = min(a.ol.brick_cnt[b], a.ol.cap_per_brick);
-    const uint64_t* slot = a.ol.slots + (size_t)b * a.ol.cap_per_brick;
-    uint2* d = ol_dst + a.ol_pre[b];
-    for (uint32_t i = lane; i < cnt; i += 64) {
-      const uint64_t c = slot[i];
-      d[i] = make_uint2((uint32_t)c, (uint32_t)(c >> 32));
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t* ex = s_ex[wid];
+  const uint32_t nslot = a.nbricks * kStreamWaves, cap = a.ol.cap_per_brick;
+  const uint32_t nwv = gridDim.x * (kFinishThreads / 64);
+  for (uint32_t g = blockIdx.x * (kFinishThreads / 64) + wid; g * 64 < nslot; g += nwv) {
+    const uint32_t s = g * 64 + (uint32_t)lane;
+    const uint32_t c = s < nslot ? min(a.ol.brick_cnt[s], cap) : 0u;
+    const uint32_t d = s < nslot ? a.ol_dst[s] : 0u;
+    const uint32_t incl = hfd::wave_incl_scan(c), total = readlane(incl, 63), d0 = readlane(d, 0);
+    ex[lane] = incl - c;
+    hfd::wave_sync();
+    for (uint32_t j = (uint32_t)lane; j < total; j += 64) {
+      uint32_t lo = 0;  // the last slot whose first cell is <= j
+#pragma unroll
+      for (uint32_t step = 32; step > 0; step >>= 1)
+        if (lo + step < 64 && ex[lo + step] <= j) lo += step;
+      const uint64_t cell = a.ol.slots[(size_t)(g * 64 + lo) * cap + (j - ex[lo])];
+      ol_dst[d0 + j] = make_uint2((uint32_t)cell, (uint32_t)(cell >> 32));
     }
+    hfd::wave_sync();
   }
   const uint32_t sp = *a.ol.spill_cnt, sp_kept = min(sp, a.ol.spill_cap);
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < sp_kept; i += gridDim.x * 256) {
+  for (uint32_t i = blockIdx.x * kFinishThreads + threadIdx.x; i < sp_kept; i += gridDim.x * kFinishThreads) {
     const uint64_t c = a.ol.spill[i];
     ol_dst[slot_total + i] = make_uint2((uint32_t)c, (uint32_t)(c >> 32));
   }
@@ -2771,32 +2885,22 @@ int launch_brick_pack(const BrickLaunch& L, const BrickCodes& bcodes, const uint
 
 template <typename T>
 int launch_brick_sample(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, uint32_t* hist, int bklen,
-                        uint32_t* ticket, uint32_t* book, uint8_t* revbook, hipStream_t st)
+                        uint32_t* ticket, uint32_t* h_hist, uint32_t* flag, uint32_t epoch, hipStream_t st)
 {
   const BrickGeom& g = L.g;
-  if ((g.ndim != 3 && g.ndim != 1) || bklen > hbook::kThreads) return (int)hipErrorInvalidValue;
+  if (g.ndim != 3 || bklen > kMaxBklen) return (int)hipErrorInvalidValue;
   const T ebx2_r = (T)(1.0 / (eb * 2)), r = (T)radius;
-  constexpr uint32_t kW1 = kSampleThreads / 64;
-  if (g.ndim == 1) {
-    const uint32_t units1 = sample_units1(g.n), stride1 = sample_stride(units1);
-    const uint32_t ns1 = (units1 + stride1 - 1) / stride1;
-    const uint32_t grid1 = std::max(1u, std::min((ns1 + kW1 - 1) / kW1, (uint32_t)L.ncu));
-    if (zz)
-      k_brick1_sample<T, true><<<grid1, kSampleThreads, 0, st>>>(in, g.n, ebx2_r, r, hist, bklen, ticket, book, revbook);
-    else
-      k_brick1_sample<T, false><<<grid1, kSampleThreads, 0, st>>>(in, g.n, ebx2_r, r, hist, bklen, ticket, book, revbook);
-    return (int)hipGetLastError();
-  }
   const uint32_t units = sample_units(L.lx, L.ly, L.lz), stride = sample_stride(units);
   const uint32_t nsamp = (units + stride - 1) / stride;
   constexpr uint32_t kW = kSampleThreads / 64;
-  const uint32_t grid = std::max(1u, std::min((nsamp + kW - 1) / kW, (uint32_t)L.ncu));
+  // two sample units per wave on a 512^3 field: half the workgroups' histogram flushes
+  const uint32_t grid = std::max(1u, std::min((nsamp + kW - 1) / kW, 2u * (uint32_t)L.ncu));
   if (zz)
     k_brick3_sample<T, true><<<grid, kSampleThreads, 0, st>>>(in, L.lx, L.ly, L.lz, ebx2_r, r, hist, bklen, ticket,
-                                                               book, revbook);
+                                                               h_hist, flag, epoch);
   else
     k_brick3_sample<T, false><<<grid, kSampleThreads, 0, st>>>(in, L.lx, L.ly, L.lz, ebx2_r, r, hist, bklen, ticket,
-                                                                book, revbook);
+                                                                h_hist, flag, epoch);
   return (int)hipGetLastError();
 }
 
@@ -2805,38 +2909,42 @@ int launch_brick_stream(const BrickLaunch& L, const T* in, double eb, int radius
                         const void* psz_tpl, const void* phf_tpl, hipStream_t st, const HostPub& pub)
 {
   const BrickGeom& g = L.g;
-  if (g.ndim != 3) return (int)hipErrorInvalidValue;
+  if (g.ndim != 3 || s.bklen > kMaxBklen) return (int)hipErrorInvalidValue;
   const T ebx2_r = (T)(1.0 / (eb * 2)), r = (T)radius;
-  StreamArgs a{L.lx, L.ly, L.lz, g.nbx, g.nby, g.nbricks, s.ol, s.book, s.bklen, s.par_nbit, s.par_entry,
-               s.bitstream, s.bs_cap, s.status, s.ticket, s.ol_pre, s.info, s.timeout};
+  StreamArgs a{L.lx,        L.ly,   L.lz,         g.nbx,        g.nby,      g.nbricks, s.ol,       s.book,
+               s.bklen,     s.par_nbit, s.par_entry, s.bitstream, s.bs_cap, s.status,  s.ticket,   s.ol_dst,
+               s.info,      s.timeout, s.gate,     s.gate_epoch, s.h_book,   s.h_revbook, s.revbook, s.rv_words,
+               s.book_flag};
+  const size_t lds = stream_lds_bytes<T>();  // dynamic: the exchange and staging areas
   static int per_cu[2] = {0, 0};
   int& pc = per_cu[sizeof(T) == 8];
   if (!pc) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k_brick3_stream<T, false>, 64 * kStreamWaves, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k_brick3_stream<T, false>, 64 * kStreamWaves, lds) !=
+            hipSuccess ||
         pc < 1)
       pc = 1;
   }
-  // persistent waves claim bricks from the ticket; every one must be resident (the look-back
-  // waits only on claimed bricks, and a claimed brick's wave is running)
-  const uint32_t grid =
-      std::max(1u, std::min((g.nbricks + kStreamWaves - 1) / kStreamWaves, (uint32_t)(pc * L.ncu)));
+  // persistent workgroups claim bricks from the ticket; every one must be resident (a look-back
+  // waits only on claimed bricks, and workgroup 0 hands every other one the codebook)
+  const uint32_t grid = std::max(1u, std::min(g.nbricks, (uint32_t)(pc * L.ncu)));
   if (zz)
-    k_brick3_stream<T, true><<<grid, 64 * kStreamWaves, 0, st>>>(in, a, ebx2_r, r);
+    k_brick3_stream<T, true><<<grid, 64 * kStreamWaves, lds, st>>>(in, a, ebx2_r, r);
   else
-    k_brick3_stream<T, false><<<grid, 64 * kStreamWaves, 0, st>>>(in, a, ebx2_r, r);
+    k_brick3_stream<T, false><<<grid, 64 * kStreamWaves, lds, st>>>(in, a, ebx2_r, r);
   if (hipError_t e = hipGetLastError()) return (int)e;
   HeaderTpl t;
   __builtin_memcpy(t.psz, psz_tpl, 176);
   __builtin_memcpy(t.phf, phf_tpl, 64);
-  const uint32_t fgrid = std::max(1u, std::min((g.nbricks + 3) / 4, 1024u));
-  k_brick3_stream_finish<<<fgrid, 256, 0, st>>>(a, t, s.archive, s.phf_offset, s.bits_rel, pub);
+  const uint32_t nslot_groups = (g.nbricks * kStreamWaves + 63) / 64;
+  const uint32_t fgrid = std::max(1u, std::min((nslot_groups + 3) / 4, 1024u));
+  k_brick3_stream_finish<<<fgrid, kFinishThreads, 0, st>>>(a, t, s.archive, s.phf_offset, s.bits_rel, pub);
   return (int)hipGetLastError();
 }
 
 template int launch_brick_sample<float>(const BrickLaunch&, const float*, double, int, bool, uint32_t*, int,
-                                        uint32_t*, uint32_t*, uint8_t*, hipStream_t);
+                                        uint32_t*, uint32_t*, uint32_t*, uint32_t, hipStream_t);
 template int launch_brick_sample<double>(const BrickLaunch&, const double*, double, int, bool, uint32_t*, int,
-                                         uint32_t*, uint32_t*, uint8_t*, hipStream_t);
+                                         uint32_t*, uint32_t*, uint32_t*, uint32_t, hipStream_t);
 template int launch_brick_stream<float>(const BrickLaunch&, const float*, double, int, bool, const BrickSingle&,
                                         const void*, const void*, hipStream_t, const HostPub&);
 template int launch_brick_stream<double>(const BrickLaunch&, const double*, double, int, bool, const BrickSingle&,

@@ -301,25 +301,34 @@ int launch_brick_pack(const BrickLaunch& L, const BrickCodes& bc, const uint32_t
                       const BrickPlanArgs& plan, uint32_t* par_nbit, uint32_t* par_entry, uint32_t* bitstream,
                       int reverse, unsigned int* overflow, hipStream_t st, const HostPub& pub = HostPub{});
 struct BrickSingle {
-  OutlierSink ol;
-  const uint32_t* book;
+  OutlierSink ol;              // one slot per (brick, y-step): cap_per_brick = the slot's cap
+  uint32_t* book;              // device book (the stream kernel's workgroup 0 writes it)
   int bklen;
   uint32_t *par_nbit, *par_entry, *bitstream;
   uint32_t bs_cap;             // bitstream capacity (cells)
   unsigned long long* status;  // nbricks words, zeroed per call
   uint32_t* ticket;            // zeroed per call
-  uint32_t* ol_pre;            // nbricks
+  uint32_t* ol_dst;            // per slot: its first cell in the archive's outlier segment
   CompressInfo* info;          // zeroed per call
   unsigned int* timeout;
   uint8_t* archive;
   size_t phf_offset, bits_rel;
+  const uint32_t* gate;        // host-mapped: reaches gate_epoch once the host's book is written
+  uint32_t gate_epoch;
+  const uint32_t* h_book;      // host-mapped book and reverse book
+  const uint32_t* h_revbook;
+  uint32_t* revbook;           // the archive's reverse book
+  int rv_words;
+  uint32_t* book_flag;         // device word (never reset)
 };
-// sampled-codebook mode (brick.hip): the sample histogram and, in the sample kernel's last
-// workgroup, the device codebook (book + the archive's reverse book); then the streaming pass
-// (+ finish: outlier segment, headers, the compress summary)
+// single-pass mode (brick.hip): the sample histogram into hist (u32[kMaxBklen * kSampleBinStride],
+// zeroed; bins one line apart); its last workgroup (ticket: kPubTicketWords words, zeroed) copies
+// it to the host-mapped h_hist and sets *flag = epoch; the host builds the codebook.  Then the
+// streaming pass, which takes the host's book behind a device-polled gate (+ finish: outlier
+// segment, headers, the compress summary)
 template <typename T>
 int launch_brick_sample(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, uint32_t* hist, int bklen,
-                        uint32_t* ticket, uint32_t* book, uint8_t* revbook, hipStream_t st);
+                        uint32_t* ticket, uint32_t* h_hist, uint32_t* flag, uint32_t epoch, hipStream_t st);
 template <typename T>
 int launch_brick_stream(const BrickLaunch& L, const T* in, double eb, int radius, bool zz, const BrickSingle& s,
                         const void* psz_tpl, const void* phf_tpl, hipStream_t st, const HostPub& pub);

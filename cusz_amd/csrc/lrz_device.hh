@@ -270,6 +270,17 @@ __device__ __forceinline__ void emit_outliers(const OutlierSink& ol, uint32_t br
   cnt += tot;
 }
 
+// emit_outliers for a lane's V consecutive elements base .. base + V - 1 (32-bit indices)
+template <int V>
+__device__ __forceinline__ void emit_outliers32(const OutlierSink& ol, uint32_t brick, uint32_t& cnt, uint32_t mask,
+                                                const float (&val)[V], uint32_t base)
+{
+  size_t idx[V];
+#pragma unroll
+  for (int k = 0; k < V; k++) idx[k] = base + (uint32_t)k;
+  emit_outliers<V>(ol, brick, cnt, mask, val, idx);
+}
+
 // Quantize one row of V elements (in-range mask), store codes, histogram, outliers.
 template <typename T, int V, bool ZZ>
 __device__ __forceinline__ void quantize_row(const T (&d)[V], T r, uint16_t* __restrict__ codes,

@@ -156,6 +156,9 @@ struct Pipeline {
   uint32_t* hist_ticket() { return reinterpret_cast<uint32_t*>(d_small + 160); }
   uint32_t* summary_ticket() { return reinterpret_cast<uint32_t*>(d_small + 196); }
   uint32_t* plan_ticket() { return reinterpret_cast<uint32_t*>(d_small + 112); }
+  // the single-pass mode's codebook flag (brick.hip k_brick3_stream): never zeroed, epoch-compared
+  uint32_t* book_flag() { return reinterpret_cast<uint32_t*>(d_small + 240); }
+  static constexpr uint32_t kStreamSlots = 8;  // outlier slots per brick in the single-pass mode (one per y-step)
   static constexpr size_t kSmallZeroBytes = 232;
   static_assert(64 + sizeof(CompressInfo) <= 112 && 112 + 36 <= 160 && 196 + 36 <= kSmallZeroBytes &&
                     kSmallZeroBytes <= 256,
@@ -805,10 +808,12 @@ struct Pipeline {
     return finish_compress(h, out, outlen);
   }
 
-  // Sampled-codebook mode (3-D bricks): the histogram of every 16th brick (+1 per bin) gives the
-  // codebook before the field is predicted; one pass then predicts and packs each brick at its
-  // look-back offset, and a finish kernel writes the outlier segment and the headers.  Codes,
-  // outliers and the reconstruction equal the exact mode's; the bitstream does not.
+  // Single-pass mode (PSZ_AMD_CODEBOOK_STREAM, 3-D bricks): the sample kernel hands the histogram
+  // of every 16th 32 x 8 x 8 unit to the host, which builds the two-queue book of sample + 1 while
+  // the streaming pass predicts its first bricks; that pass takes the book behind a device-polled
+  // gate, sizes each brick (one workgroup per brick), takes its offset by a look-back and writes
+  // its rows straight to the archive; a finish kernel writes the outlier segment and the headers.
+  // Codes, outliers and the reconstruction equal the exact mode's; the bitstream does not.
   template <typename T>
   int compress_sampled(psz_header* h, const T* in, uint8_t** out, size_t* outlen)
   {
@@ -831,9 +836,12 @@ struct Pipeline {
       h->rc.eb *= (mm[1] - mm[0]);
     }
     const double eb = h->rc.eb;
-    // look-back status words live in the per-brick histogram area (unused in this mode)
+    // the look-back status words (one per brick), then the outlier count and destination of each
+    // (brick, y-step) slot, live in the per-brick histogram area (unused in this mode: 2 KB a brick)
     unsigned long long* status = reinterpret_cast<unsigned long long*>(d_bhist);
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_zero(regions({{d_hist, nullptr, (size_t)bklen * 4},
+    uint32_t* slot_cnt = reinterpret_cast<uint32_t*>(status + g.nbricks);
+    uint32_t* slot_dst = slot_cnt + (size_t)g.nbricks * kStreamSlots;
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_zero(regions({{d_shist, nullptr, (size_t)kMaxBklen * kSampleBinStride * 4},
                                                         {d_small, nullptr, kSmallZeroBytes},
                                                         {status, nullptr, (size_t)g.nbricks * 8}}),
                                                stream));
@@ -844,11 +852,32 @@ struct Pipeline {
     const int bsub = g.W, bpar = (int)g.nchunks;
     const size_t nbit_rel = 128 + rvbk, entry_rel = nbit_rel + 4 * (size_t)bpar;
     const size_t bits_rel = entry_rel + 4 * (size_t)bpar;
-    // sample histogram; its last workgroup builds the codebook on the device (book_device.hh):
-    // the book, and the reverse book straight into the archive
-    CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_sample<T>(bl, in, eb, radius, zz, d_hist, bklen, hist_ticket(), d_book,
-                                                          d_archive + phf_off + 128, stream));
+    // the sample histogram; its last workgroup publishes it to the host (flag 2)
+    const uint32_t eh = ++epoch;
+    CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_sample<T>(bl, in, eb, radius, zz, d_shist, bklen, hist_ticket(), h_hist(),
+                                                          const_cast<uint32_t*>(flag(2)), eh, stream));
     mark(2);
+    // the host's two-queue book of sample + 1 opens the gate the streaming pass polls; it must
+    // open on every path out of here, or the stream (and every later call on it) waits forever
+    const uint32_t eg = ++gate_epoch;
+    struct GateGuard {
+      volatile uint32_t* f;
+      uint32_t e;
+      bool armed;
+      ~GateGuard()
+      {
+        if (armed) __atomic_store_n(f, e, __ATOMIC_RELEASE);
+      }
+    } guard{flag(5), eg, true};
+    auto build_book = [&]() -> int {
+      int fs = wait_flag(2, eh);
+      if (!fs) build_codebook_twoqueue(h_hist(), bklen, 1u, h_book(), h_revbook());
+      __atomic_store_n(flag(5), eg, __ATOMIC_RELEASE);
+      guard.armed = false;
+      return fs;
+    };
+    if (!gate)  // (diagnostic switch: the book before the launch)
+      if (int fs = build_book()) return fs;
     mark(3);
     h->vle_sublen = bsub;
     h->vle_pardeg = bpar;
@@ -860,7 +889,7 @@ struct Pipeline {
     ph.entry[0] = 0, ph.entry[1] = 128, ph.entry[2] = (uint32_t)nbit_rel, ph.entry[3] = (uint32_t)entry_rel;
     ph.entry[4] = (uint32_t)bits_rel;
     const size_t chunks = std::max((size_t)pardeg, (size_t)g.nchunks);
-    BrickSingle sg{OutlierSink{d_slots, d_brick_cnt, d_spill, spill_cnt(), brick_cap(), spill_cap, nullptr},
+    BrickSingle sg{OutlierSink{d_slots, slot_cnt, d_spill, spill_cnt(), brick_cap() / kStreamSlots, spill_cap, nullptr},
                    d_book,
                    bklen,
                    reinterpret_cast<uint32_t*>(d_archive + phf_off + nbit_rel),
@@ -869,17 +898,26 @@ struct Pipeline {
                    (uint32_t)std::min<size_t>(bitstream_cells_cap() + chunks, 0xFFFFFFFFu),
                    status,
                    &info()->ticket,
-                   d_ub,
+                   slot_dst,
                    info(),
                    timeout(),
                    d_archive,
                    phf_off,
-                   bits_rel};
+                   bits_rel,
+                   const_cast<const uint32_t*>(flag(5)),
+                   eg,
+                   h_book(),
+                   reinterpret_cast<const uint32_t*>(h_revbook()),
+                   reinterpret_cast<uint32_t*>(d_archive + phf_off + 128),
+                   (int)(rvbk / 4),
+                   book_flag()};
     const HostPub sp{readback_regions(), const_cast<uint32_t*>(flag(3)), ++epoch, summary_ticket()};
     CUSZ_AMD_HIP_CHECK((hipError_t)launch_brick_stream<T>(bl, in, eb, radius, zz, sg, h, &ph, stream, sp));
     summary_epoch = sp.epoch;
     mark(4);
     mark(5);
+    if (guard.armed)
+      if (int fs = build_book()) return fs;
     return finish_compress(h, out, outlen);
   }
 

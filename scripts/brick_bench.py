@@ -3,7 +3,7 @@
 
 Times compress and decompress with HIP events on the manager's stream (CUSZ_AMD_LIB selects a
 variant library, e.g. one built with a timing-experiment switch).
-Usage: python scripts/brick_bench.py [--dims 512x512x512] [--reps 10] [--f64]
+Usage: python scripts/brick_bench.py [--dims 512x512x512] [--reps 10] [--f64] [--codebook stream]
 """
 import argparse
 import os
@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--eb", type=float, default=1e-4)
     ap.add_argument("--f64", action="store_true")
+    ap.add_argument("--codebook", default="default", choices=["default", "exact", "sampled", "stream"])
     ap.add_argument("--dbg", default="0", help="(ignored; kept for old command lines)")
     a = ap.parse_args()
     dims = tuple(int(v) for v in a.dims.split("x"))
@@ -37,6 +38,8 @@ def main():
     st = torch.cuda.current_stream()
     r = cz.Resource(cz.F8 if a.f64 else cz.F4, dims, stream=st.cuda_stream)
     r.enable_timing(True)
+    if a.codebook != "default":
+        r.set_codebook({"exact": cz.CODEBOOK_EXACT, "sampled": cz.CODEBOOK_SAMPLED, "stream": cz.CODEBOOK_STREAM}[a.codebook])
     ptr, nb, _ = r.compress(d_in.data_ptr(), a.eb)
     print(f"layout={r.internals().layout} sublen={r.header.vle_sublen} CR={n * d_in.element_size() / nb:.3f}")
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
