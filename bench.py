@@ -614,7 +614,7 @@ def bench_sharded(args, world, rank, dist, dev):
     fields = datagen.nyx_fields_torch(full, device=dev, z0=z0, z1=z0 + sl.dims[2])
     stream = torch.cuda.current_stream(dev)
     res = [cz.Resource(cz.F4, sl.dims, stream=stream.cuda_stream) for _ in fields]
-    hists = torch.empty((len(fields), 1025), dtype=torch.int32, device=dev)
+    hists = torch.empty((len(fields), 1026), dtype=torch.int32, device=dev)
     total_bytes = 6 * full[0] * full[1] * full[2] * 4
     state = {"scratch": None}
 

@@ -260,7 +260,9 @@ __device__ __forceinline__ void finish_unit(const OutlierSink& ol, const BrickCo
   if (sample) {
     __builtin_amdgcn_s_waitcnt(0);  // this wave's sample atomics have completed
     uint32_t prev = 0;
-    if (lane == 0) prev = __hip_atomic_fetch_add(sp.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // release / acquire at agent scope: the wave completing the sample sees every sample brick's
+    // atomics by the memory model, not only by the hardware's ordering (once per sample brick)
+    if (lane == 0) prev = __hip_atomic_fetch_add(sp.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if ((uint32_t)__builtin_amdgcn_readfirstlane((int)prev) == sp.count - 1 && sp.pub_flag) {
       // the sample is complete: this wave hands it to the host (agent-scope reads: every
       // sample brick's atomics have completed before its count)

@@ -229,7 +229,8 @@ struct Pipeline {
     ndim = ndim_of(l);
     elem_bytes = dt == F8 ? 8 : 4;
     // the 2-D Lorenzo kernels address one row through a 32-bit buffer range: a row of 2 GiB or
-    // more is a shape this build does not take (such a field compresses as 1-D)
+    // more is a shape this build does not take (creation fails with this status; the caller
+    // reshapes such a field to 1-D)
     if (ndim == 2 && l.x * (size_t)elem_bytes >= 0x80000000ull) return PSZ_ABORT_UNSUPPORTED_DIMENSION;
     stream = (hipStream_t)st;
     CUSZ_AMD_HIP_CHECK(hipGetDevice(&device));

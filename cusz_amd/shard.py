@@ -142,28 +142,44 @@ def compress_fields_sharded(resources, fields, eb, dist, mode=0, radius=512, dev
     ValueError otherwise): RCCL orders the all-reduce after the scans and the finish after the
     all-reduce on that stream, so no host synchronisation is needed between the phases.  The u32 histogram sums are
     reduced as int32 (the bit pattern is the u32 sum: every count is < 2^32).
-    A slab with more outliers than its capacity (past the reference's 10 %) makes every rank's
-    finish warn through the summed overflow word (column 2 radius of `hists`); every rank then
-    repeats its scans, the all-reduce and its finishes once, with the grown capacity.
+    Each histogram row carries two words after the counts, summed by the same all-reduce: the
+    slab's overflow word (outlier cells past its capacity, written by the scan) and a failure
+    word.  A rank whose scan fails (e.g. a manager broken by a failed allocation) still joins the
+    all-reduce, with a zeroed row and its failure word set, so that no peer waits for it: every
+    rank then sees the failure and raises.  A slab with more outliers than its capacity (past the
+    reference's 10 %) makes every rank's finish warn through the summed overflow word; every
+    rank then repeats its scans, the all-reduce and its finishes once, with the grown capacity.
+    A finish that fails otherwise raises after that repeat (which its peers may be waiting for).
+    `hists`: optional [fields, 2 radius + 2] int32 scratch on the managers' device (one of
+    2 radius + 1 columns is replaced by an internal one).
     Returns [(archive_ptr, nbytes)] (device archives, valid until the manager's next compress)."""
     import torch
 
-    from . import PSZ_WARN_OUTLIER_TOO_MANY, PszError
+    from . import PSZ_AMD_ERR_DEVICE, PSZ_WARN_OUTLIER_TOO_MANY, PszError
 
     bklen = 2 * radius
     f = len(resources)
     check_streams(resources, device if device is not None else (fields[0].device if fields else None))
     ebs = [eb * r for r in global_value_ranges(resources, fields, dist)] if mode == 1 else [eb] * f
-    if hists is None:
-        hists = torch.empty((f, bklen + 1), dtype=torch.int32, device=device)
-    assert hists.shape[-1] == bklen + 1, "histogram rows hold 2 radius counts + the overflow word"
+    if hists is None or hists.shape[-1] != bklen + 2:
+        hists = torch.empty((f, bklen + 2), dtype=torch.int32, device=device)
+    failure = None
+    out = []
     for attempt in range(2):
+        scan_failed = False
         for i, (r, t) in enumerate(zip(resources, fields)):
-            r.compress_scan(t.data_ptr(), ebs[i], hists[i].data_ptr(), 0, radius)
+            try:
+                r.compress_scan(t.data_ptr(), ebs[i], hists[i].data_ptr(), 0, radius)
+                hists[i, bklen + 1] = 0
+            except PszError as e:
+                failure = failure or e
+                scan_failed = True
+                hists[i].zero_()
+                hists[i, bklen + 1] = 1  # this rank's scan failed: the peers learn it from the sum
         if dist is not None and dist.get_world_size() > 1:
-            allreduce_histograms(hists, dist)  # the overflow words are summed with the counts
-        out, again, failure = [], False, None
-        for i, r in enumerate(resources):
+            allreduce_histograms(hists, dist)  # the overflow and failure words are summed with the counts
+        out, again = [], False
+        for i, r in enumerate(resources if not scan_failed else []):
             try:
                 ptr, nb, _ = r.compress_finish(hists[i].data_ptr())
             except PszError as e:
@@ -174,22 +190,27 @@ def compress_fields_sharded(resources, fields, eb, dist, mode=0, radius=512, dev
                     continue
                 failure = failure or e
                 # any other failure: when the summed overflow word makes the other ranks repeat,
-                # this rank repeats with them (their all-reduce would wait for it forever), then
-                # raises
+                # this rank repeats with them (their all-reduce would wait for it forever); its
+                # scan on the repeat fails too (a broken manager) and tells the peers so
                 if not attempt and retry_needed(hists[i], bklen):
                     again = True
                 continue
             out.append((ptr, nb))
-        if failure is not None and not again:
-            raise failure
+        # a failed scan anywhere: every rank raises (read after the finishes, which have waited
+        # for the device anyway: no extra host synchronisation between the phases)
+        if scan_failed or int(hists[:, bklen + 1].max().item()) != 0:
+            raise failure or PszError(PSZ_AMD_ERR_DEVICE, "compress_scan on a peer rank")
         if not again:
-            return out
+            break
+    if failure is not None:
+        raise failure
     return out
 
 
 def retry_needed(hist_row, bklen: int) -> bool:
-    """The summed overflow word of a reduced histogram row (u32[2 radius + 1]): nonzero when some
-    slab of this field overflowed its outlier list, so every rank repeats the scan."""
+    """The summed overflow word of a reduced histogram row (u32[2 radius + 2]: counts, overflow
+    word, failure word): nonzero when some slab of this field overflowed its outlier list, so
+    every rank repeats the scan."""
     return int(hist_row[bklen].item()) != 0
 
 

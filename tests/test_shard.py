@@ -192,3 +192,86 @@ def test_merge_rejects_truncated_part(oracle):
         with pytest.raises(cz.PszError) as e:
             cz.merge_archives([p[:cut]], dims)
         assert e.value.status == cz.PSZ_AMD_ERR_BAD_ARCHIVE
+
+
+class _FakeSlab:
+    """A manager stand-in for the collective logic of shard.compress_fields_sharded (no GPU):
+    the scan writes a histogram row (+ an overflow word), the finish returns a fake archive or
+    raises as scripted per attempt."""
+
+    def __init__(self, hists, row, scan_fail=(), finish_status=None, overflow=0):
+        self.hists, self.row, self.calls = hists, row, 0
+        self.scan_fail, self.finish_status, self.overflow = scan_fail, finish_status or {}, overflow
+
+    def compress_scan(self, ptr, eb, hist_ptr, mode, radius):
+        from cusz_amd import PSZ_AMD_ERR_DEVICE, PszError
+
+        k = self.calls
+        self.calls += 1
+        if k in self.scan_fail:
+            raise PszError(PSZ_AMD_ERR_DEVICE, "compress_scan")
+        bklen = 2 * radius
+        self.hists[self.row, :bklen] = 1
+        self.hists[self.row, bklen] = self.overflow if k == 0 else 0
+
+    def compress_finish(self, hist_ptr):
+        from cusz_amd import PszError
+
+        st = self.finish_status.get(self.calls - 1)
+        if st is not None:
+            raise PszError(st, "compress_finish")
+        return 1234, 56, None
+
+
+def _retry_worker(rank, world, port, case, q):
+    from cusz_amd import PSZ_AMD_ERR_DEVICE, PSZ_WARN_OUTLIER_TOO_MANY
+    from cusz_amd import shard
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    radius = 4
+    hists = torch.zeros((1, 2 * radius + 2), dtype=torch.int32)
+    if case == "scan_fails":  # rank 1's manager is broken: its scan fails before the all-reduce
+        r = _FakeSlab(hists, 0, scan_fail=(0,) if rank == 1 else ())
+    elif case == "overflow":  # rank 0's slab overflows: every rank warns, both repeat, then succeed
+        st = {0: PSZ_WARN_OUTLIER_TOO_MANY}
+        r = _FakeSlab(hists, 0, finish_status=st, overflow=5 if rank == 0 else 0)
+    else:  # "finish_fails": rank 0's finish fails hard while the overflow makes rank 1 repeat;
+        # rank 0 repeats too, its scan then fails (a broken manager), and both raise
+        st = {0: PSZ_AMD_ERR_DEVICE if rank == 0 else PSZ_WARN_OUTLIER_TOO_MANY}
+        r = _FakeSlab(hists, 0, scan_fail=(1,) if rank == 0 else (), finish_status=st, overflow=3 if rank == 1 else 0)
+    x = torch.zeros(8)
+    try:
+        out = shard.compress_fields_sharded([r], [x], 1e-4, dist, radius=radius, hists=hists)
+        q.put((rank, "ok", len(out), r.calls))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, "raised", getattr(e, "status", None), r.calls))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", ["scan_fails", "overflow", "finish_fails"])
+def test_sharded_retry_is_collective(case):
+    """No rank waits forever in the histogram all-reduce: a rank whose scan fails still joins it
+    and every rank raises; an overflow repeats on every rank together."""
+    from cusz_amd import PSZ_AMD_ERR_DEVICE
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29800 + {"scan_fails": 0, "overflow": 7, "finish_fails": 13}[case] + os.getpid() % 500
+    ps = [ctx.Process(target=_retry_worker, args=(r, 2, port, case, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {}
+    for _ in range(2):
+        rank, what, st, calls = q.get(timeout=120)
+        res[rank] = (what, st, calls)
+    for p in ps:
+        p.join(timeout=60)
+    if case == "overflow":
+        assert res[0] == ("ok", 1, 2) and res[1] == ("ok", 1, 2)
+    elif case == "scan_fails":
+        assert res[0][0] == "raised" and res[1][0] == "raised"
+        assert res[0][1] == PSZ_AMD_ERR_DEVICE and res[1][1] == PSZ_AMD_ERR_DEVICE
+    else:
+        assert res[0][:2] == ("raised", PSZ_AMD_ERR_DEVICE) and res[1][:2] == ("raised", PSZ_AMD_ERR_DEVICE)
+        assert res[0][2] == 2 and res[1][2] == 2  # both repeated the scan once
