@@ -8,9 +8,14 @@ C-ABI.  value = field bytes / step time (max over ranks).
 
 GPUs (one process per GPU).  `--gpus N` with N > 1 and no WORLD_SIZE in the environment
 re-launches this script under torch.distributed.run (before any GPU call in the parent); under
-torchrun WORLD_SIZE must equal N.  With N ranks the ONE field is split into tile-aligned z-slabs
-(8-plane multiples, shard.plan_slabs) -- strong scaling -- and a step is the sharded compress of
-SURVEY.md §8e:
+torchrun WORLD_SIZE must equal N.  The path partitions into independent fields / tiles (SURVEY.md
+§8e), so by default (`--scaling weak`) every rank compresses and decompresses its OWN 512^3 field
+(the config's recipe, seed per rank) with no collective in the timed steps; value = N x field
+bytes / the slowest rank's step time.  The per-rank archives are then gathered to rank 0 (exact-
+size grouped ncclSend/ncclRecv over xGMI) outside the timed steps (host_phases_ms.gather,
+value_incl_gather), and the root decompresses every rank's archive against that rank's field.
+`--scaling strong` splits ONE field into tile-aligned z-slabs (8-plane multiples,
+shard.plan_slabs) instead, and a step is the sharded compress of SURVEY.md §8e:
   pass 1 per slab (psz_amd_compress_scan_float) -> ONE all-reduce of the u32[1024 + 1] histogram
   (RCCL) -> finish per slab with the shared codebook (psz_amd_compress_finish) -> every rank
   decompresses its own slab (its archive stays resident on its GPU).
@@ -66,10 +71,16 @@ def parse():
                          "step reads an input the previous steps left in the 256 MiB Infinity Cache; "
                          "the same-field rate is reported beside it")
     ap.add_argument("--rel", action="store_true", help="config 4: value-range relative bound (r2r) instead of abs")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="N > 1: weak = an independent field per rank (the default: the path partitions, no "
+                         "collective in the timed steps); strong = one field in z-slabs with a shared codebook")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (PCIe) path timing")
     ap.add_argument("--profile-only", action="store_true", help="few steps, no baselines (rocprof)")
     ap.add_argument("--no-other-modes", action="store_true", help="skip the other codebook modes' timings")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1 process group: nccl (= RCCL over xGMI); gloo is a diagnostic to rehearse the "
+                         "multi-rank path with several ranks on ONE GPU (collectives staged through host memory)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the launch, rank plumbing and the collectives (gloo) only")
     return ap.parse_args()
@@ -107,8 +118,8 @@ def main() -> int:
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        torch.cuda.set_device(local % torch.cuda.device_count())  # (gloo rehearsal: ranks may share a GPU)
+        dist.init_process_group(args.backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -198,9 +209,9 @@ def bench_field(args, world, rank, dist, dev):
     mode, predictor, tdt = cfg[2], cfg[3], cfg[4]
     esz = 8 if tdt == torch.float64 else 4
     n_full = dims[0] * dims[1] * dims[2]
-    # the spline archive has an anchor segment the slab merge does not rebase: with several
-    # ranks, config 5 runs one independent field per rank (weak scaling) instead
-    sharded = world > 1 and predictor != cz.Spline
+    # weak scaling (the default): an independent field per rank.  strong: one field in z-slabs --
+    # not for spline (its archive has an anchor segment the slab merge does not rebase)
+    sharded = world > 1 and predictor != cz.Spline and args.scaling == "strong"
     weak = world > 1 and not sharded
     slab = shard.plan_slabs(dims, world)[rank] if sharded else shard.Slab(rank, 0, dims, 0)
     my_dims, n = slab.dims, slab.count
@@ -254,10 +265,14 @@ def bench_field(args, world, rank, dist, dev):
         t1 = time.perf_counter()
         # RCCL gather of the per-rank archives to the root: output collection, not part of the
         # timed compress+decompress (each rank's archive stays resident and is decompressed
-        # there); timed in the phase pass and done before the merge check
-        if sharded and (gather or acc is not None):
+        # there); timed in the phase pass and done before the root's checks
+        if world > 1 and (gather or acc is not None):
             view, state["scratch"] = archive_view(ptr, nb, dev, state["scratch"])
-            state["parts"] = shard.gather_to_root(view, dist, 0)
+            if args.backend == "gloo":  # (rehearsal: gloo moves host tensors)
+                parts = shard.gather_to_root(view.cpu(), dist, 0)
+                state["parts"] = None if parts is None else [q.to(dev) for q in parts]
+            else:
+                state["parts"] = shard.gather_to_root(view, dist, 0)
         t2 = time.perf_counter()
         r.decompress(ptr, nb, d_out.data_ptr())
         if acc is not None:
@@ -322,7 +337,8 @@ def bench_field(args, world, rank, dist, dev):
     ptr, nb = step(rot=False, gather=True)  # field 0's archive for what follows (CR, merge, roofline)
     torch.cuda.synchronize()
     if dist is not None:
-        t = torch.tensor([dt, dt_same, acc[0], acc[1], acc[2]], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt, dt_same, acc[0], acc[1], acc[2]], device=dev if args.backend == "nccl" else "cpu",
+                         dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, dt_same, acc[0], acc[1], acc[2] = t.tolist()
     ms_per_step = 1e3 * dt / args.steps
@@ -349,6 +365,27 @@ def bench_field(args, world, rank, dist, dev):
             merged_ok = bool(e_full <= 1.001 * eb_abs + ulp)
             r_full.close()
             del out, d_arch, d_full
+        barrier()
+    elif weak:
+        # the root decompresses every rank's gathered archive against that rank's field (the
+        # recipe is deterministic: regenerated from the rank's seed)
+        parts = state["parts"]
+        if rank == 0:
+            ok = True
+            for k, p in enumerate(parts):
+                hdr = cz.psz_header.from_buffer_copy(p[:176].cpu().numpy().tobytes())
+                rk = cz.Resource(cz.F4 if esz == 4 else cz.F8, dims, predictor, stream=stream.cuda_stream, header=hdr)
+                out = torch.empty(n_full, dtype=tdt, device=dev)
+                rk.decompress(p.data_ptr(), p.numel(), out.data_ptr())
+                fk = make_field(seed - rank + k)
+                torch.cuda.synchronize()
+                e_k = (out.double() - fk.double()).abs().max().item()
+                bound = 1.001 * hdr.rc.eb + ulp  # (the header's eb is absolute: Rel mode scaled it)
+                ok = ok and e_k <= bound
+                rk.close()
+                del out, fk
+            merged_ok = bool(ok)
+            arch_bytes_total = sum(int(p.numel()) for p in parts)
         barrier()
     ratio = esz * n_full / arch_bytes_total if sharded else nbytes_in / nb
 
@@ -488,7 +525,7 @@ def bench_field(args, world, rank, dist, dev):
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak" if weak else "strong",
+            "scaling": "strong" if sharded or (world == 1 and args.scaling == "strong") else "weak",
             "vs_baseline": None,
             "dtype": "f64" if esz == 8 else "f32",
             "data": f"synthetic (SURVEY.md §8d config-{args.config} recipe" + (", seed per rank)" if weak else ")"),
@@ -499,7 +536,8 @@ def bench_field(args, world, rank, dist, dev):
                        "field_bytes": esz * n_full, "per_rank_bytes": nbytes_in,
                        "parallelism": (f"dp{world} (tile-aligned z-slabs of one field: histogram all-reduce; "
                                        "archive gather to rank 0 outside the timed steps)") if sharded else
-                                      (f"dp{world} (independent fields)" if weak else "single GPU")},
+                                      (f"dp{world} (an independent field per rank, no collective in the timed "
+                                       "steps; archives gathered to rank 0 outside them)" if weak else "single GPU")},
             "compress_gbps": round(nbytes_in / (comp_ms * 1e-3) / 1e9, 2) if comp_ms > 0 else None,
             "decompress_gbps": round(nbytes_in / (decomp_ms * 1e-3) / 1e9, 2) if decomp_ms > 0 else None,
             "compress_roofline_frac": round(nbytes_in / (comp_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if comp_ms > 0 else None,
@@ -512,7 +550,7 @@ def bench_field(args, world, rank, dist, dev):
                                "decompress_to_idle": round(td_ms, 4)},
             "field_compress_call_gbps": round(total_bytes / (tc_ms * 1e-3) / 1e9, 2) if tc_ms > 0 else None,
             "field_compress_gather_gbps": round(total_bytes / ((tc_ms + tg_ms) * 1e-3) / 1e9, 2) if tc_ms > 0 else None,
-            "value_incl_gather": (round(total_bytes / ((ms_per_step + tg_ms) * 1e-3) / 1e9, 2) if sharded else None),
+            "value_incl_gather": (round(total_bytes / ((ms_per_step + tg_ms) * 1e-3) / 1e9, 2) if world > 1 else None),
             "compression_ratio": round(ratio, 3),
             "stages_ms": {k: round(float(st[i]), 4) for k, i in
                           [("predict", cz.T_PREDICT), ("book", cz.T_BOOK), ("encode", cz.T_ENCODE),
@@ -532,6 +570,9 @@ def bench_field(args, world, rank, dist, dev):
         if sharded:
             line["merged_archive_bytes"] = arch_bytes_total
             line["merged_decompress_ok"] = merged_ok
+        elif weak:
+            line["gathered_archive_bytes"] = arch_bytes_total
+            line["gathered_decompress_ok"] = merged_ok
         print(json.dumps(line), flush=True)
     r.close()
 
