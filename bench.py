@@ -564,6 +564,13 @@ def bench_field(args, world, rank, dist, dev):
                          else "two-queue book of pass 1's brick sample + 1 (host, mid-pass)"
                          if ino.layout == cz.LAYOUT_BRICK and (dims[2] > 1 or dims[1] == 1)
                          else "reference heap book of the full histogram (host)"),
+            # `value` is measured with the default (SAMPLED) codebook mode: unless the line above
+            # names the reference heap book, the archive's Huffman book is NOT the reference
+            # encoder's (same quantization codes and decompressed field, different bitstream);
+            # the EXACT mode's reference-identical archive is timed beside it
+            "archive_reference_identical": bool(
+                predictor != cz.Spline and not sharded and not (ino.layout == cz.LAYOUT_BRICK and (dims[2] > 1 or dims[1] == 1))),
+            "value_exact_codebook": (other_modes or {}).get("exact", {}).get("value"),
             "other_codebook_modes": other_modes,
             "max_abs_err": err,
         }

@@ -98,6 +98,29 @@ def test_sharded_device_book(oracle, dims, world, layout):
     assert err <= 1.001 * eb + 2.0 ** -23 * float(np.abs(data).max())
 
 
+@pytest.mark.parametrize("dims,world", [((256, 32, 40), 3), ((512, 24, 64), 4)])
+def test_sharded_default_mode_decodes_like_whole_field(dims, world):
+    """Default (SAMPLED) mode: the whole-field compress takes a sampled host book and the sharded
+    finish a device book of the reduced histogram, so the archives differ; the quantization codes
+    and outliers do not, so both decompress to the IDENTICAL field, within the bound, and the
+    sizes stay within 1 %."""
+    data = datagen.smooth3d_np(dims, 17)
+    eb = 1e-4
+    single, r = _whole(data, dims, eb, np.float32, cz.LAYOUT_BRICK, 0, codebook=cz.CODEBOOK_SAMPLED)
+    merged = _sharded(data, dims, world, eb, np.float32, cz.LAYOUT_BRICK, 0, codebook=cz.CODEBOOK_SAMPLED)
+    assert abs(len(merged) - len(single)) <= 0.01 * len(single)
+    outs = []
+    for arch in (single, merged):
+        d_arch = torch.frombuffer(bytearray(arch), dtype=torch.uint8).cuda()
+        out = torch.full((data.size,), float("nan"), dtype=torch.float32, device="cuda")
+        rx = cz.Resource(cz.F4, dims, header=cz.psz_header.from_buffer_copy(arch[:176]))
+        rx.decompress(d_arch.data_ptr(), len(arch), out.data_ptr())
+        sync()
+        outs.append(out.cpu().numpy())
+    np.testing.assert_array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+    assert np.abs(outs[0].astype(np.float64) - data.astype(np.float64)).max() <= 1.001 * eb
+
+
 def test_scan_then_finish_equals_compress():
     dims = (256, 24, 16)
     data = datagen.smooth3d_np(dims, 7)
