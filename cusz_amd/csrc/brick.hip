@@ -1823,330 +1823,6 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
     for (int i = 0; i < 16; i++) atomicAdd(&g_brick_prof[i], pc[i]);
 #endif
 }
-#if CUSZ_AMD_DEC_PAIR
-// ---- paired decoder (3-D fused path, two bricks per wave) -------------------------------------
-// The compact chunk loop decodes every brick row in lockstep blocks, so a brick costs its slowest
-// row: the (y 0, z 0) row of each 8^3 tile row (x-only prediction, the longest codes: ~246 steps
-// against ~157 for the others, §7).  Here a wave decodes TWO bricks at once and each lane two
-// chunks, one per brick, in independent chains: lane l holds row l of brick A and row (l + 9) mod
-// 64 of brick B, so each brick's heavy row shares its lane with a light (inner) row of the other
-// brick -- a lane's block costs the sum of its two rows (at most ~246 + 154 for two bricks instead
-// of 2 x 246) -- and the two chains' table and ring reads overlap.  A chain that has finished its
-// block (or waits for ring words) steps on a zero entry, storing into a junk slot, so both chains
-// run in one instruction stream.  LDS per wave: two rings, a 128-row tile (rows 64 b + r), two
-// bricks' cell values and row starts: 4 waves per CU, one per SIMD.
-constexpr uint32_t kPairRows = 128;
-constexpr size_t kP4Ring = (size_t)(kRing4 + 2) * 256;                 // one chain's ring (+ mirror, junk)
-constexpr size_t kP4Tile = 2 * kP4Ring;                                 // tile: 128 rows of kTP4 u16
-constexpr size_t kP4Cells = kP4Tile + (size_t)kPairRows * kTP4 * 2;     // 2 x kCellCap values
-constexpr size_t kP4Rows = kP4Cells + (size_t)2 * kCellCap * 4;         // 2 x (65 starts + 64 carries)
-constexpr size_t kP4WaveBytes = kP4Rows + (size_t)2 * (65 + 64) * 4;
-#ifndef CUSZ_AMD_DEC_PAIR_WAVES
-#define CUSZ_AMD_DEC_PAIR_WAVES 4
-#endif
-constexpr int kDecPairWaves = CUSZ_AMD_DEC_PAIR_WAVES;
-static_assert(sizeof(hfd::Tab4) + kDecPairWaves * kP4WaveBytes <= 160 * 1024, "LDS");
-constexpr uint32_t kTab4Zero = (1u << 12) + hfd::kL2Cap4 - 1;  // an entry that is always 0
-
-struct PairChain {
-  uint32_t* ring;  // this lane's slot 0 (slot s at ring[64 s])
-  uint16_t* row;   // the chunk's tile row
-  uint32_t vbase;  // byte offset of the chunk in the bitstream
-  uint32_t nwords;
-};
-
-// Both chains of every lane through W / kBlk blocks; recon(blk) after each block (both bricks),
-// blk_start(blk) before it, pro() while the first words land.  first[c][0..1]: chain c's first 8
-// words, loaded by the caller.
-template <class Pro, class BlkStart, class Recon>
-__device__ __forceinline__ void decode_pairs4(const hfd::Tab4& tb, const hfd::DecRegs4& rg, __amdgpu_buffer_rsrc_t rbits,
-                                              uint32_t ubk, PairChain (&ch)[2], const uint32_t (&nbit)[2],
-                                              const uint32_t (&vlen)[2], uint16_t* const (&junk)[2], Pro&& pro,
-                                              BlkStart&& blk_start, Recon&& recon, const u32x4 (&first)[2][2])
-{
-  constexpr uint32_t W = 256;
-  uint32_t A[2], Bw[2], pos8[2], npos[2], ltop[2], ctop[2], rdy[2];
-  uint16_t* tp[2];
-  u32x4 pa[2], pb[2];
-  bool fa[2], fb[2];
-  pro();
-#pragma unroll
-  for (int c = 0; c < 2; c++) {
-    uint32_t* ring = ch[c].ring;
-    const u32x4 a0 = first[c][0], a1 = first[c][1];
-    ring[0] = a0.x, ring[64] = a0.y, ring[2 * 64] = a0.z, ring[3 * 64] = a0.w;
-    ring[4 * 64] = a1.x, ring[5 * 64] = a1.y, ring[6 * 64] = a1.z, ring[7 * 64] = a1.w;
-    ring[16 * 64] = a0.x;  // mirror of slot 0
-    A[c] = 0, Bw[c] = a0.x;
-    pos8[c] = 8u * 511u, npos[c] = 0;
-    ltop[c] = 8, ctop[c] = 8;
-    rdy[c] = ctop[c] >= ch[c].nwords ? 0xFFFFFFFFu : 256u * ctop[c] + kRdy4;
-    tp[c] = ch[c].row;
-    fa[c] = fb[c] = false;
-  }
-  auto issue = [&](int c, u32x4& p, bool& f) {
-    const bool ok = ltop[c] < ch[c].nwords && ltop[c] + 4u <= (pos8[c] >> 8);
-    p = __builtin_amdgcn_raw_buffer_load_b128(rbits, (int)(ok ? ch[c].vbase + ltop[c] * 4u : kOOB), 0, 0);
-    f = ok;
-    ltop[c] += ok ? 4u : 0u;
-  };
-  auto consume = [&](int c, const u32x4& p, bool& f) {
-    if (f) {
-      uint32_t* sl = ch[c].ring + (ctop[c] & (kRing4 - 1u)) * 64;
-      sl[0] = p.x, sl[64] = p.y, sl[128] = p.z, sl[192] = p.w;
-      if ((ctop[c] & (kRing4 - 1u)) == 0u) ch[c].ring[16 * 64] = p.x;
-      ctop[c] += 4u;
-      rdy[c] = ctop[c] >= ch[c].nwords ? 0xFFFFFFFFu : 256u * ctop[c] + kRdy4;
-    }
-    f = false;
-  };
-  auto advance = [&](int c, uint32_t e) {
-    const uint32_t sy = e & hfd::kEnt4SymMask;
-    tp[c][0] = (uint16_t)sy;
-    asm volatile("" ::: "memory");  // two u16 stores: merged they would be an unaligned b32
-    tp[c][1] = (uint16_t)(sy >> 16);
-    tp[c] = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(tp[c]) + hfd::ent4_adv(e));
-    const uint32_t b = hfd::ent4_bits(e);
-    pos8[c] += b << 3;
-    npos[c] -= b;
-    const uint32_t* rr = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(ch[c].ring) + (pos8[c] & 0xF00u));
-    A[c] = rr[0];
-    Bw[c] = rr[64];
-  };
-  auto window = [&](int c) { return __builtin_amdgcn_alignbit(A[c], Bw[c], npos[c]); };
-
-  for (int blk = 0; blk < (int)(W / kBlk); blk++) {
-    blk_start(blk);
-    const uint32_t done = (uint32_t)blk * kBlk;
-    uint16_t* tlim[2];
-#pragma unroll
-    for (int c = 0; c < 2; c++) tlim[c] = ch[c].row + (vlen[c] > done ? min((uint32_t)kBlk, vlen[c] - done) : 0u);
-    auto quarter = [&]() {
-      bool act[2];
-#pragma unroll
-      for (int c = 0; c < 2; c++) act[c] = tp[c] < tlim[c] && pos8[c] < rdy[c];
-      if (act[0] || act[1]) {
-        // an idle chain steps on the zero entry (no symbol, no bits) and stores into its junk slot
-        uint16_t* keep[2];
-#pragma unroll
-        for (int c = 0; c < 2; c++) {
-          keep[c] = tp[c];
-          tp[c] = act[c] ? tp[c] : junk[c];
-        }
-        uint32_t e[2] = {0, 0};
-#pragma unroll
-        for (int st = 0; st < kF; st++) {
-#pragma unroll
-          for (int c = 0; c < 2; c++) e[c] = tb.e[act[c] ? hfd::tab4_index(rg, window(c)) : kTab4Zero];
-#pragma unroll
-          for (int c = 0; c < 2; c++) advance(c, e[c]);
-        }
-        const bool lng0 = act[0] && e[0] == 0, lng1 = act[1] && e[1] == 0;
-        if (__builtin_amdgcn_ballot_w64(lng0 || lng1)) {  // a code longer than 16 bits stopped a chain
-          if (lng0) advance(0, hfd::lookup_long4(tb, rg, window(0), ubk));
-          if (lng1) advance(1, hfd::lookup_long4(tb, rg, window(1), ubk));
-        }
-#pragma unroll
-        for (int c = 0; c < 2; c++) tp[c] = act[c] ? tp[c] : keep[c];
-      }
-    };
-    auto short_any = [&]() { return __builtin_amdgcn_ballot_w64(tp[0] < tlim[0] || tp[1] < tlim[1]) != 0; };
-    issue(0, pa[0], fa[0]);
-    issue(1, pa[1], fa[1]);
-    quarter();
-    quarter();
-    issue(0, pb[0], fb[0]);
-    issue(1, pb[1], fb[1]);
-    quarter();
-    quarter();
-    bool odd = false;
-    for (;;) {
-      consume(0, pa[0], fa[0]);
-      consume(1, pa[1], fa[1]);
-      issue(0, pa[0], fa[0]);
-      issue(1, pa[1], fa[1]);
-      quarter();
-      if (!short_any()) {
-        odd = true;
-        break;
-      }
-      quarter();
-      if (!short_any()) {
-        odd = true;
-        break;
-      }
-      consume(0, pb[0], fb[0]);
-      consume(1, pb[1], fb[1]);
-      issue(0, pb[0], fb[0]);
-      issue(1, pb[1], fb[1]);
-      quarter();
-      if (!short_any()) break;
-      quarter();
-      if (!short_any()) break;
-    }
-    if (odd) consume(0, pb[0], fb[0]), consume(1, pb[1], fb[1]);  // drain in issue order
-    consume(0, pa[0], fa[0]);
-    consume(1, pa[1], fa[1]);
-    consume(0, pb[0], fb[0]);
-    consume(1, pb[1], fb[1]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a group no lane consumed may be in flight
-    hfd::wave_sync();
-    // symbols decoded past the block end move to its front (held in registers across the
-    // reconstruction, which may use the tile as scratch)
-    uint32_t ovs[2][kF + 1];
-#pragma unroll
-    for (int c = 0; c < 2; c++)
-#pragma unroll
-      for (int i = 0; i <= kF; i++) ovs[c][i] = reinterpret_cast<const uint32_t*>(ch[c].row)[kBlk / 2 + i];
-    recon(blk);
-    hfd::wave_sync();
-#pragma unroll
-    for (int c = 0; c < 2; c++) {
-#pragma unroll
-      for (int i = 0; i <= kF; i++) reinterpret_cast<uint32_t*>(ch[c].row)[i] = ovs[c][i];
-      tp[c] = tp[c] >= ch[c].row + kBlk ? tp[c] - kBlk : ch[c].row;
-    }
-    hfd::wave_sync();
-  }
-}
-
-template <typename T, bool ZZ, bool BUF>
-__global__ void __launch_bounds__(64 * kDecPairWaves)
-k_brick3_decode2(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const uint8_t* __restrict__ revbook,
-                 int bklen, const uint32_t* __restrict__ par_nbit, const uint32_t* __restrict__ par_entry, T* out,
-                 uint32_t lx, uint32_t ly, uint32_t lz, T ebx2, T r, uint32_t nbx, uint32_t nby, uint32_t nbricks,
-                 BrickOutliers ol)
-{
-  __shared__ hfd::Tab4 tb;
-  extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
-  hfd::build_tab4(tb, revbook, bklen);
-  const hfd::DecRegs4 rg = hfd::load_dec_regs4(tb);
-  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* wbase = dsm + (size_t)wid * kP4WaveBytes;
-  uint16_t* tile = reinterpret_cast<uint16_t*>(wbase + kP4Tile);
-  uint32_t* cval = reinterpret_cast<uint32_t*>(wbase + kP4Cells);
-  uint32_t* rows = reinterpret_cast<uint32_t*>(wbase + kP4Rows);
-  BrickCells bc[2] = {{cval, 1, rows, rows + 65}, {cval + kCellCap, 1, rows + 129, rows + 129 + 65}};
-  const bool ranked = !ZZ && (ol.ncell == 0 || *ol.unsorted != ol.epoch);
-  const __amdgpu_buffer_rsrc_t rbits =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(bitstream), 0, (int)(bs_words * 4u), (int)kBufRsrcW3);
-  uint32_t* ring_lane0 = reinterpret_cast<uint32_t*>(wbase) + lane;
-  uint16_t* const junk[2] = {reinterpret_cast<uint16_t*>(ring_lane0 + 17 * 64),
-                             reinterpret_cast<uint16_t*>(ring_lane0 + kP4Ring / 4 + 17 * 64)};
-  const size_t plane = (size_t)lx * ly;
-  constexpr uint32_t W = 256;
-  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
-  const uint32_t npairs = (nbricks + 1) / 2;
-  // chain 0: row l of brick A; chain 1: row (l + 9) mod 64 of brick B (the heavy rows, 0, meet
-  // inner rows: l = 0 takes B's row 9, l = 55 takes B's row 0 and A's row 55)
-  const uint32_t rowc[2] = {(uint32_t)lane, ((uint32_t)lane + 9u) & 63u};
-
-  struct Next {
-    uint32_t nbit[2], entry[2], cb[2], ce[2];
-    bool live[2];
-  };
-  auto fetch1 = [&](uint32_t b, uint32_t rw, uint32_t& nbit, uint32_t& entry, uint32_t& cb, uint32_t& ce, bool& live) {
-    live = false, nbit = 0, entry = 0, cb = 0, ce = 0;
-    if (b >= nbricks) return;
-    const uint32_t bx = b % nbx, t = b / nbx, by = t % nby, bz = t / nby;
-    const uint32_t ry = rw >> 3, rz = rw & 7u;
-    live = by * 8 + ry < ly && bz * 8 + rz < lz;
-    if (live) {
-      const size_t ci = ((size_t)(bz * 8 + rz) * ly + (by * 8 + ry)) * nbx + bx;
-      nbit = par_nbit[ci], entry = par_entry[ci];
-    }
-    if (ranked && ol.ncell) cb = ol.bstart[b], ce = ol.bstart[b + 1];
-  };
-  auto fetch = [&](uint32_t p) {
-    Next x;
-    fetch1(2 * p, rowc[0], x.nbit[0], x.entry[0], x.cb[0], x.ce[0], x.live[0]);
-    fetch1(2 * p + 1, rowc[1], x.nbit[1], x.entry[1], x.cb[1], x.ce[1], x.live[1]);
-    return x;
-  };
-  u32x4 first[2][2];
-  uint2 pcell[2][2];  // per brick: cells cb + lane and cb + 64 + lane
-  auto prefetch = [&](const Next& x) {
-#pragma unroll
-    for (int c = 0; c < 2; c++) {
-      first[c][0] = __builtin_amdgcn_raw_buffer_load_b128(rbits, (int)(x.live[c] ? x.entry[c] * 4u : kOOB), 0, 0);
-      first[c][1] = __builtin_amdgcn_raw_buffer_load_b128(rbits, (int)(x.live[c] ? x.entry[c] * 4u + 16u : kOOB), 0, 0);
-#pragma unroll
-      for (int k = 0; k < 2; k++) {
-        const uint32_t j = x.cb[c] + (uint32_t)lane + 64u * k;
-        pcell[c][k] = ranked && j < x.ce[c] ? make_uint2(ol.cells[2 * (size_t)j], ol.cells[2 * (size_t)j + 1]) : make_uint2(0, 0);
-      }
-    }
-  };
-  const uint32_t p0 = npairs <= nw ? (uint32_t)wid * gridDim.x + blockIdx.x : blockIdx.x * (blockDim.x >> 6) + wid;
-  Next nx = fetch(p0);
-  prefetch(nx);
-  for (uint32_t p = p0; p < npairs; p += nw) {
-    const Next cur = nx;
-    const u32x4 f2[2][2] = {{first[0][0], first[0][1]}, {first[1][0], first[1][1]}};
-    const uint2 cp[2][2] = {{pcell[0][0], pcell[0][1]}, {pcell[1][0], pcell[1][1]}};
-    PairChain ch[2];
-    uint32_t nbitc[2], vlen[2];
-#pragma unroll
-    for (int c = 0; c < 2; c++) {
-      ch[c].ring = ring_lane0 + (size_t)c * (kP4Ring / 4);
-      ch[c].row = tile + ((size_t)c * 64 + rowc[c]) * kTP4;
-      nbitc[c] = cur.live[c] ? cur.nbit[c] : 0u;
-      ch[c].vbase = (cur.live[c] ? cur.entry[c] : 0u) * 4u;
-      ch[c].nwords = cur.live[c] ? (nbitc[c] + 31u) >> 5 : 0u;
-      vlen[c] = cur.live[c] ? W : 0u;
-    }
-    // the bricks' outlier cells [cb, ce): per-row counts -> row starts; values into LDS
-    auto pro_one = [&](BrickCells& bk, uint32_t* cv, uint32_t cb, uint32_t ce, uint2 c0, uint2 c1) {
-      const uint32_t nc = ce - cb;
-      bk.row_start[lane] = 0;
-      hfd::wave_sync();
-      for (uint32_t j = (uint32_t)lane; j < nc; j += 64) {
-        const uint2 cell = j < 64u    ? c0
-                           : j < 128u ? c1
-                                      : make_uint2(ol.cells[2 * (size_t)(cb + j)], ol.cells[2 * (size_t)(cb + j) + 1]);
-        const uint32_t idx = cell.y;
-        const uint32_t yz = idx / lx;  // y + ly z
-        atomicAdd(&bk.row_start[((yz % ly) & 7u) * 8u + ((yz / ly) & 7u)], 1u);
-        if (nc <= kCellCap) cv[j] = cell.x;
-      }
-      hfd::wave_sync();
-      const uint32_t cr = bk.row_start[lane];
-      const uint32_t incl = hfd::wave_incl_scan(cr);
-      bk.row_start[lane] = incl - cr;
-      if (lane == 63) bk.row_start[64] = incl;
-      bk.carry[lane] = 0;
-      bk.val = nc <= kCellCap ? cv : ol.cells + 2 * (size_t)cb;
-      bk.vstride = nc <= kCellCap ? 1u : 2u;
-    };
-    auto pro = [&]() {
-      if (!ranked) return;
-      pro_one(bc[0], cval, cur.cb[0], cur.ce[0], cp[0][0], cp[0][1]);
-      pro_one(bc[1], cval + kCellCap, cur.cb[1], cur.ce[1], cp[1][0], cp[1][1]);
-    };
-    auto recon = [&](int blk) {
-      if (blk == (int)(W / kBlk) - 1) prefetch(nx);  // the next pair (fetched during this block)
-      auto recon1 = [&](uint32_t b, const uint16_t* tl, BrickCells* bk) {
-        if (b >= nbricks) return;  // (uniform)
-        const uint32_t bx = b % nbx, t = b / nbx, by = t % nby, bz = t / nby;
-        const uint32_t y0 = by * 8, z0 = bz * 8;
-        const uint32_t nyv = min(8u, ly - y0), nzv = min(8u, lz - z0);
-        const size_t base_elem = (size_t)z0 * plane + (size_t)y0 * lx + (size_t)bx * W + (size_t)blk * kBlk;
-        if (ranked)
-          recon_block<T, ZZ, BUF, kTP4, true>(tl, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane, bk);
-        else
-          recon_block<T, ZZ, BUF, kTP4, false>(tl, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane);
-      };
-      recon1(2 * p, tile, &bc[0]);
-      recon1(2 * p + 1, tile + 64 * kTP4, &bc[1]);
-    };
-    auto blk_start = [&](int blk) {
-      if (blk == (int)(W / kBlk) - 1) nx = fetch(p + nw);
-    };
-    decode_pairs4(tb, rg, rbits, (uint32_t)bklen, ch, nbitc, vlen, junk, pro, blk_start, recon, f2);
-  }
-}
-
-#endif
 // ---- 1-D: fused decode + reconstruct -------------------------------------------------------
 // A wave owns a unit of 64 tiles of 1024 (4 chunks of 256 each); lane l owns tile 64 u + l and
 // decodes its four chunks in four phases (phase p: chunk 4 t + p).  After each block of 64
@@ -3323,19 +2999,11 @@ int launch_brick_decode(const BrickLaunch& L, const uint32_t* bitstream, size_t 
   const size_t plane = (size_t)L.lx * L.ly;
   const bool buf = (7 * plane + 7 * (size_t)L.lx + (size_t)kBlk) * sizeof(T) < (1ull << 31);
   const uint32_t bw = (uint32_t)bs_words;
-#if CUSZ_AMD_DEC_PAIR
-  const size_t lds = (size_t)kDecPairWaves * kP4WaveBytes;  // dynamic part
-#define DEC_LAUNCH(ZZ, BUF)                                                                                     \
-  k_brick3_decode2<T, ZZ, BUF><<<L.ncu, 64 * kDecPairWaves, lds, st>>>(bitstream, bw, revbook, bklen, par_nbit, par_entry, \
-                                                                  out, L.lx, L.ly, L.lz, ebx2, r, g.nbx, g.nby,       \
-                                                                  g.nbricks, ol)
-#else
   const size_t lds = (size_t)kDec4Waves * kD4WaveBytes;  // dynamic part
 #define DEC_LAUNCH(ZZ, BUF)                                                                                     \
   k_brick3_decode<T, ZZ, BUF><<<L.ncu, 64 * kDec4Waves, lds, st>>>(bitstream, bw, revbook, bklen, par_nbit, par_entry, \
                                                                   out, L.lx, L.ly, L.lz, ebx2, r, g.nbx, g.nby,       \
                                                                   g.nbricks, ol)
-#endif
   if (zz) {
     if (buf) DEC_LAUNCH(true, true); else DEC_LAUNCH(true, false);
   }
