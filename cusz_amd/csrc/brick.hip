@@ -1715,8 +1715,6 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
 {
   __shared__ hfd::Tab4 tb;  // static: table addresses fold into the ds offsets
   extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
-  hfd::build_tab4(tb, revbook, bklen);
-  const hfd::DecRegs4 rg = hfd::load_dec_regs4(tb);
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* wbase = dsm + (size_t)wid * kD4WaveBytes;
   uint16_t* tile = reinterpret_cast<uint16_t*>(wbase + kD4Tile);
@@ -1767,7 +1765,9 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
   // wave w of every workgroup takes brick w * grid + block, spreading them over every CU (one per
   // SIMD for 1024 bricks) instead of filling half the CUs two waves per SIMD
   const uint32_t b0 = nbricks <= nw ? (uint32_t)wid * gridDim.x + blockIdx.x : blockIdx.x * (blockDim.x >> 6) + wid;
-  Next nx = fetch(b0);
+  Next nx = fetch(b0);  // (lands while the tables are built)
+  hfd::build_tab4(tb, revbook, bklen);
+  const hfd::DecRegs4 rg = hfd::load_dec_regs4(tb);
   prefetch(nx);
   for (uint32_t brick = b0; brick < nbricks; brick += nw) {
     BPROF(pc[0]++; tp = __builtin_readcyclecounter();)

@@ -363,7 +363,16 @@ struct Tab4 {
 };
 
 // Cooperative build by the whole workgroup (ends with a barrier); same decoding rule as
-// build_tables (hf_kernels.cuhip.inl:351-365), entries in the compact format.
+// build_tables (hf_kernels.cuhip.inl:351-365), entries in the compact format.  Every decoder
+// workgroup builds it before its first step, so it is kept cheap (≈ 2x fewer VALU than one
+// counting decode per symbol slot):
+//  * the failing-length count compares (win >> 1) with uniform thresholds first[k] << (31 - k)
+//    (SGPRs; 0 past the longest code), one compare + one add per length;
+//  * one decode per 12-bit window: the first codes go to a u16 scratch table (length << 10 |
+//    symbol, 0 = longer than 12 bits) in the L2 area; an L1 entry's second code is that table's
+//    entry for the window shifted past the first code (the zero-filled low bits never decide a
+//    code that fits the remaining bits: prefix-free), so the second decode is one LDS read;
+//  * then the L2 entries overwrite the scratch.
 __device__ __forceinline__ void build_tab4(Tab4& t, const uint8_t* revbook, int bklen)
 {
   constexpr int B = 12;
@@ -379,28 +388,47 @@ __device__ __forceinline__ void build_tab4(Tab4& t, const uint8_t* revbook, int 
     if (tid == 0) t.maxl = (uint32_t)maxl;
   }
   __syncthreads();
-  uint32_t first[32];
+  // (win >> (32 - k)) < first[k]  <=>  (win >> 1) < first[k] << (31 - k)   (first[k] <= 2^k)
+  uint32_t T[kLmax + 1];
 #pragma unroll
-  for (int k = 0; k < 32; k++) first[k] = t.first[k];
-  const uint32_t ub = (uint32_t)bklen;
-  for (uint32_t i = tid; i < (1u << B); i += nt) {
-    const uint32_t v = i << (32 - B);
-    uint32_t s0, s1, e = 0;
-    const uint32_t l0 = tab_decode1(v, first, maxl, t.base, t.keys, ub, s0);
-    if (l0 <= (uint32_t)B) {
-      const uint32_t rest = B - l0;
-      const uint32_t l1 = rest ? tab_decode1(v << l0, first, maxl, t.base, t.keys, ub, s1) : 99u;
-      e = l1 <= rest ? ent4_pack(2, l0 + l1, s0, s1) : ent4_pack(1, l0, s0, 0);
-    }
-    t.e[i] = e;
+  for (int k = 1; k <= kLmax; k++) {
+    const uint32_t f = t.first[k];
+    T[k] = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)(k > maxl ? 0u : (f >= (1u << k) ? 0xFFFFFFFFu : f << (31 - k))));
   }
-  const uint32_t P = maxl > B ? min(first[B], 1u << B) : 0u;
+  const uint32_t ub = (uint32_t)bklen, ml = (uint32_t)maxl;
+  auto decode1 = [&](uint32_t v, uint32_t& sym) -> uint32_t {
+    const uint32_t h = v >> 1;
+    uint32_t l = 1;
+#pragma unroll
+    for (int k = 1; k <= kLmax; k++) l += h < T[k] ? 1u : 0u;
+    l = min(l, ml);
+    sym = t.keys[min(t.base[l] + (v >> (32 - l)), ub - 1)];
+    return l;
+  };
+  uint16_t* s1 = reinterpret_cast<uint16_t*>(t.e + (1 << B));  // 4096 u16 = the L2 area
+  static_assert(kL2Cap4 * 2 >= (1 << B), "scratch fits the L2 area");
+  for (uint32_t i = tid; i < (1u << B); i += nt) {
+    uint32_t s;
+    const uint32_t l = decode1(i << (32 - B), s);
+    s1[i] = (uint16_t)(l <= (uint32_t)B ? (l << 10) | s : 0u);
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < (1u << B); i += nt) {
+    const uint32_t a = s1[i];
+    const uint32_t l0 = a >> 10, rest = B - l0;
+    const uint32_t b = a && rest ? s1[(i << l0) & ((1u << B) - 1)] : 0u;
+    const uint32_t l1 = b >> 10;
+    t.e[i] = !a ? 0u : (b && l1 <= rest ? ent4_pack(2, l0 + l1, a & 1023u, b & 1023u) : ent4_pack(1, l0, a & 1023u, 0));
+  }
+  __syncthreads();
+  const uint32_t P = maxl > B ? min(t.first[B], 1u << B) : 0u;
   const uint32_t n2 = min(P << (kL2Bits - B), (uint32_t)kL2Cap4 - 1);
   for (uint32_t q = tid; q < (uint32_t)kL2Cap4; q += nt) {
     uint32_t e = 0;
     if (q < n2) {
       uint32_t s0;
-      const uint32_t l = tab_decode1(q << (32 - kL2Bits), first, maxl, t.base, t.keys, ub, s0);
+      const uint32_t l = decode1(q << (32 - kL2Bits), s0);
       if (l <= (uint32_t)kL2Bits) e = ent4_pack(1, l, s0, 0);
     }
     t.e[(1 << B) + q] = e;
