@@ -156,6 +156,35 @@ struct StepLoader {
       __builtin_memcpy(reinterpret_cast<char*>(&dst[0]) + 16 * h, &v, 16);
     }
   }
+  // The same loads with the brick's address work done once per brick (BrickRows): per row only
+  // the in-brick offset and two compares, instead of the brick coordinates, the 64-bit origin and
+  // the descriptor again for every row (pass 1: ~50 scalar instructions and the SGPR spills they
+  // cause, per row).
+  struct BrickRows {
+    __amdgpu_buffer_rsrc_t rs;  // at the brick's origin, 8 planes long
+    uint32_t nyv, nzv;          // rows y < nyv, z < nzv lie in the field (0: past the last brick)
+  };
+  __device__ __forceinline__ BrickRows rows_of(uint32_t it) const
+  {
+    const bool live = it < nbricks;
+    const uint32_t b = live ? brick_of(it) : 0u, bx = b % nbx, t = b / nbx, by = t % nby, bz = t / nby;
+    const T* origin = in + (size_t)bz * 8 * plane + (size_t)by * 8 * lx + (size_t)bx * (64 * V);
+    const uint32_t span = (uint32_t)(8 * plane * sizeof(T));  // < 2^31 (brick_geom)
+    return {__builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(origin), 0, (int)span, 0x00020000),
+            live ? min(8u, ly - by * 8) : 0u, live ? min(8u, lz - bz * 8) : 0u};
+  }
+  __device__ __forceinline__ void issue_row(const BrickRows& br, uint32_t y, uint32_t z, T (&dst)[V]) const
+  {
+    const uint32_t span = (uint32_t)(8 * plane * sizeof(T));
+    const bool ok = y < br.nyv && z < br.nzv;
+    const uint32_t off = ok ? (z * (uint32_t)plane + y * lx) * (uint32_t)sizeof(T) + lane * (V * sizeof(T)) : span;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int h = 0; h < (int)(V * sizeof(T) / 16); h++) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(br.rs, (int)(off + 16 * h), 0, CUSZ_AMD_SCAN_LOAD_AUX);
+      __builtin_memcpy(reinterpret_cast<char*>(&dst[0]) + 16 * h, &v, 16);
+    }
+  }
   __device__ __forceinline__ void issue(uint32_t it, int y, T (&dst)[8][V]) const
   {
     if (it >= nbricks) return;
@@ -315,8 +344,11 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
   uint32_t it = blockIdx.x * kBrickWaves + wid;  // iteration; its brick in the pass-1 order (BrickSample)
   const T bias = r - (T)bcs.c0;  // the byte-first path (below)
   T q[D][V];
+  {
+    const auto b0 = ld.rows_of(it < nunits ? pass1_brick(it, sp) : nbricks);
 #pragma unroll
-  for (int j = 0; j < D; j++) ld.issue_row(it < nunits ? pass1_brick(it, sp) : nbricks, j, q[j]);
+    for (int j = 0; j < D; j++) ld.issue_row(b0, (uint32_t)j >> 3, (uint32_t)j & 7u, q[j]);
+  }
   static_assert(kUnitBricks == 1, "one row mask per unit");
   uint64_t rowmask = 0;  // rows of the brick stored as u16 (uniform)
   for (; it < nunits; it += nw) {
@@ -325,6 +357,7 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
     const uint32_t bend = u + 1;
     for (uint32_t brick = u; brick < bend; brick++) {
       const uint32_t bnext = it + nw < nunits ? pass1_brick(it + nw, sp) : nbricks;  // next brick of the stream
+      const auto rc = ld.rows_of(brick), rn = ld.rows_of(bnext);
       const uint32_t bx = brick % nbx, t = brick / nbx, by = t % nby, bz = t / nby;
       const uint32_t x0 = bx * (64 * V) + lane * V, y0 = by * 8, z0 = bz * 8;
       uint16_t* cbrick = bcs.c16 + (size_t)brick * 64 * (64 * V) + (size_t)lane * V;
@@ -335,16 +368,19 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
       for (int z = 0; z < 8; z++)
 #pragma unroll
         for (int k = 0; k < V; k++) bprev[z][k] = (T)0;
+      static_assert(D == 8, "one y-step in flight: the rows ahead are one y-step of one brick");
 #pragma unroll 1
-      for (int r0 = 0; r0 < 64; r0 += D)  // not unrolled: instruction cache
+      for (int r0 = 0; r0 < 64; r0 += D) {  // not unrolled: instruction cache
+        const bool last = r0 + D >= 64;  // the rows ahead are the next brick's first y-step
+        const auto ahead = last ? rn : rc;
+        const uint32_t ya = last ? 0u : (uint32_t)(r0 + D) >> 3;
 #pragma unroll
         for (int j = 0; j < D; j++) {
           const int row = r0 + j, z = j & 7, y = row >> 3;
           T p[V];
 #pragma unroll
           for (int k = 0; k < V; k++) p[k] = dround(q[j][k] * ebx2_r);
-          if (row + D < 64) ld.issue_row(brick, row + D, q[j]);
-          else ld.issue_row(bnext, row + D - 64, q[j]);
+          ld.issue_row(ahead, ya, (uint32_t)j & 7u, q[j]);  // row + D: y-step ya of `ahead`, z = j
           const uint32_t gy = y0 + (uint32_t)y;
           // z-diff (lrz_c.cuhip.inl:341-352 order: z, then x inside the 8-wide tile, then y)
           T a[V];
@@ -422,6 +458,7 @@ k_brick3_scan(const T* __restrict__ in, uint32_t lx, uint32_t ly, uint32_t lz, T
             emit_outliers<V>(ol, u, cnt, mask, olv, idx);  // one slot per unit
           }
         }
+      }
     }
     finish_unit(ol, bcs, u, cnt, rowmask, s_hist, s_wg, bhist, hs, lane, sp, sp.hist && it < sp.count);
   }

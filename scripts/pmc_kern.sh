@@ -4,7 +4,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 export CUSZ_AMD_NO_GATE=1  # counter passes serialise dispatches (see pmc_config.sh)
-re=$1; tag=$2; lib=${3:-cusz_amd/lib}; drv=${4:-scripts/brick_bench.py}; shift 4 2>/dev/null; extra="$@"
+re=$1; tag=$2; lib=${3:-cusz_amd/lib}; drv=${4:-scripts/brick_bench.py}; shift $(( $# < 4 ? $# : 4 )); extra="$@"
 mkdir -p gpurun_out/$tag
 i=0
 for ctr in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
