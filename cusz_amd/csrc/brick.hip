@@ -1154,12 +1154,23 @@ __device__ __forceinline__ double dpp0(double v)
   const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xf, 0xf, false);
   return __builtin_bit_cast(double, (unsigned long long)(uint32_t)lo | ((unsigned long long)(uint32_t)hi << 32));
 }
+// Each step must stay one v_add_*_dpp: left alone, the SLP vectorizer pairs two z rows' steps
+// into v_mov_b32_dpp x 2 (plus two movs of the 0 `old`) + v_pk_add_f32, 5 instructions for 2;
+// the empty asm makes every step's result opaque to it.
+template <typename T>
+__device__ __forceinline__ void no_slp(T& t)
+{
+  if constexpr (sizeof(T) == 4) asm("" : "+v"(t));  // (not volatile: free to schedule)
+}
 template <typename T>
 __device__ __forceinline__ T x_scan8i(T t)
 {
   t = t + dpp0<0x112>(t);  // row_shr:2 = column x - 1
+  no_slp(t);
   t = t + dpp0<0x114>(t);  // row_shr:4 = column x - 2
+  no_slp(t);
   t = t + dpp0<0x118>(t);  // row_shr:8 = column x - 4
+  no_slp(t);
   return t;
 }
 
