@@ -22,8 +22,8 @@
 //                            (= chunk) into LDS cells -> store at region + running offset;
 //                            par_nbit / par_entry; the unit's outlier slot is copied out.
 //   decompress (k_brick3_decode): one wave per brick, one chunk per lane decoded in x-blocks of
-//                            64 symbols into an LDS code tile; the block is reconstructed
-//                            (reference scan order) and stored as whole rows.
+//                            32 symbols (f32; 64 for f64) into an LDS code tile; the block is
+//                            reconstructed (reference scan order) and stored as whole rows.
 // Single-pass mode (k_brick3_sample, k_brick3_stream, k_brick3_stream_finish): the book comes
 // from a 1/16 sample of 32 x 8 x 8 units before the field is predicted, and one pass -- a
 // workgroup per brick, a wave per y-step -- predicts, sizes (look-back over the bricks) and packs
@@ -1302,6 +1302,125 @@ __device__ __forceinline__ void recon_block(const uint16_t* tile, T* out, size_t
   }
 }
 
+// lanes 32-63: lane - 32's x; lanes 0-31: -0.0 (v_permlane32_swap: lanes 32-63 of the first
+// operand trade with lanes 0-31 of the second)
+template <typename T>
+__device__ __forceinline__ T from_lower_half(T x)
+{
+  if constexpr (sizeof(T) == 4) {
+    const auto s = __builtin_amdgcn_permlane32_swap(0x80000000u, __builtin_bit_cast(uint32_t, x), false, false);
+    return __builtin_bit_cast(T, (uint32_t)s[0]);
+  }
+  else {
+    const uint64_t u = __builtin_bit_cast(uint64_t, x);
+    const auto lo = __builtin_amdgcn_permlane32_swap(0u, (uint32_t)u, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(0x80000000u, (uint32_t)(u >> 32), false, false);
+    return __builtin_bit_cast(T, (uint64_t)(uint32_t)lo[0] | ((uint64_t)(uint32_t)hi[0] << 32));
+  }
+}
+
+// 32-column blocks (the 12-wave decoder, k_brick3_decode32): lane l reconstructs column
+// rcol(l mod 32) of y-steps 4 h .. 4 h + 3, h = l / 32, so both halves' x and z scans run
+// together.  The y running sum keeps the reference's order: every lane sums its four values
+// from a start value, -0.0 in the lower half (-0.0 + v == v for every v, so s_0 = v_0 exactly)
+// and, in the upper half, the lower half's s_3 of the same column (v_permlane32_swap).
+// Outliers: as recon_block, each row's zero codes ranked among the 32 lanes of its half.
+template <typename T, bool ZZ, bool BUF, int TP, bool CELLS>
+__device__ __forceinline__ void recon_block32(const uint16_t* tile, T* out, size_t plane, uint32_t lx, uint32_t nyv,
+                                              uint32_t nzv, size_t base_elem, T r, T ebx2, int lane,
+                                              const BrickCells* bc = nullptr)
+{
+  T* base = out + base_elem;  // element (x0, y0, z0) of this block
+  const uint32_t hl = (uint32_t)lane >> 5, l32 = (uint32_t)lane & 31u;
+  const uint32_t col = rcol(l32);
+  const uint32_t ybase = 4u * hl;
+  T v[4][8];
+#pragma unroll
+  for (int yy = 0; yy < 4; yy++) {
+    const uint32_t y = ybase + (uint32_t)yy;
+    const bool yok = y < nyv;
+    uint32_t cd[8];
+#pragma unroll
+    for (int z = 0; z < 8; z++) cd[z] = tile[(y * 8 + (uint32_t)z) * TP + col];
+#pragma unroll
+    for (int z = 0; z < 8; z++) {
+      if constexpr (ZZ)
+        v[yy][z] = (T)zz_dec((uint16_t)cd[z]);
+      else
+        v[yy][z] = (T)cd[z] - r;
+    }
+    const uint32_t mn = min(min(min(cd[0], cd[1]), min(cd[2], cd[3])), min(min(cd[4], cd[5]), min(cd[6], cd[7])));
+    if (__builtin_amdgcn_ballot_w64(yok && mn == 0u)) {  // a zero code in this y step (rare)
+      if constexpr (CELLS) {  // outliers: ranked cells of the brick
+#pragma unroll
+        for (int z = 0; z < 8; z++) {
+          const uint64_t m = __builtin_amdgcn_ballot_w64(yok && cd[z] == 0u);
+          if (m && (uint32_t)z < nzv) {
+            const uint32_t mh = (uint32_t)(m >> (32u * hl));  // this half's row
+            const uint32_t row = y * 8u + (uint32_t)z;
+            if (mh) {
+              const uint32_t c0 = bc->row_start[row] + bc->carry[row], ce = bc->row_start[row + 1];
+              const uint32_t j = c0 + col_rank((uint64_t)mh, l32);
+              if (cd[z] == 0u) v[yy][z] = (j < ce ? (T)__builtin_bit_cast(float, bc->val[j * bc->vstride]) : T(0)) - r;
+            }
+            hfd::wave_sync();
+            if (l32 == 0 && mh) bc->carry[row] += (uint32_t)__builtin_popcount(mh);
+          }
+        }
+      }
+      else {  // outliers: their values were scattered into out
+#pragma unroll
+        for (int z = 0; z < 8; z++) {
+          if (yok && cd[z] == 0u && (uint32_t)z < nzv) {
+            const T o = base[(size_t)z * plane + (size_t)y * lx + col];
+            v[yy][z] = ZZ ? o + T(0) : o - r;
+          }
+        }
+      }
+    }
+  }
+  // y running sums: the lower half's s_3 (computed by every lane, used by the upper half)
+  T c[8];
+#pragma unroll
+  for (int z = 0; z < 8; z++) {
+    T u = v[0][z];
+#pragma unroll
+    for (int yy = 1; yy < 4; yy++) u = u + v[yy][z];
+    c[z] = from_lower_half<T>(u);
+  }
+#pragma unroll
+  for (int yy = 0; yy < 4; yy++) {
+    const uint32_t y = ybase + (uint32_t)yy;
+    T t[8];
+#pragma unroll
+    for (int z = 0; z < 8; z++) {
+      c[z] = c[z] + v[yy][z];
+      t[z] = x_scan8i<T>(c[z]);
+    }
+#pragma unroll
+    for (int d = 1; d < 8; d *= 2)
+#pragma unroll
+      for (int z = 7; z >= d; z--) t[z] = t[z] + t[z - d];
+#pragma unroll
+    for (int z = 0; z < 8; z++) t[z] = t[z] * ebx2;
+    if (y < nyv) {
+      if constexpr (BUF) {
+        const __amdgpu_buffer_rsrc_t ro = rsrc(base + (size_t)yy * lx);
+        const uint32_t voff = (col + hl * 4u * lx) * (uint32_t)sizeof(T);
+#pragma unroll
+        for (int z = 0; z < 8; z++)
+          if ((uint32_t)z < nzv) buf_store<T>(t[z], ro, voff, (uint32_t)((size_t)z * plane * sizeof(T)));
+      }
+      else {
+        T* rowb = base + (size_t)y * lx;
+#pragma unroll
+        for (int z = 0; z < 8; z++)
+          if ((uint32_t)z < nzv) rowb[(size_t)z * plane + col] = t[z];
+      }
+    }
+  }
+}
+
 #ifdef CUSZ_AMD_DEC_PROFILE
 // diagnostic build (psz_amd_debug_brick_profile): per-phase clocks and counts summed over waves:
 // 0 bricks, 1 brick-start cycles (cells, loads and their wait), 2 decode-loop cycles, 3 drain
@@ -1587,7 +1706,7 @@ struct DecWave4 {
 // One chunk per lane (bits at byte vbase, nbit bits, vlen <= W symbols; a dead lane decodes
 // nothing; its first 8 words in first[0..1]) in W / kBlk blocks into the tile; recon(blk) after
 // each block, blk_start(blk) before it, pro() while the first words are written.
-template <class Pro, class BlkStart, class Recon>
+template <int BLK = kBlk, int TP = kTP4, class Pro, class BlkStart, class Recon>
 __device__ __forceinline__ void decode_chunks4(const hfd::Tab4& tb, const hfd::DecRegs4& rg, const DecWave4& dw,
                                                bool live, uint32_t vbase, uint32_t nbit, uint32_t vlen, Pro&& pro,
                                                BlkStart&& blk_start, Recon&& recon BPROF_P4, uint32_t W,
@@ -1619,7 +1738,7 @@ __device__ __forceinline__ void decode_chunks4(const hfd::Tab4& tb, const hfd::D
   // a quarter reaches at most 4 x 16 + 27 bits: the lane steps only if their words are in
   // (pos8 < 8 (32 ctop + 388))
   uint32_t rdy = ctop >= nwords ? 0xFFFFFFFFu : 256u * ctop + kRdy4;
-  uint16_t* tp = dw.tile + lane * kTP4;
+  uint16_t* tp = dw.tile + lane * TP;
   u32x4 pa, pb;  // groups in flight
   bool fa = false, fb = false;
   BPROF(hfd::wave_sync(); tk = __builtin_readcyclecounter(); pc[1] += tk - tp0; tp0 = tk;)
@@ -1674,11 +1793,11 @@ __device__ __forceinline__ void decode_chunks4(const hfd::Tab4& tb, const hfd::D
   auto window = [&]() { return __builtin_amdgcn_alignbit(A, Bw, npos); };
 #endif
 
-  for (int blk = 0; blk < (int)(W / kBlk); blk++) {
+  for (int blk = 0; blk < (int)(W / BLK); blk++) {
     blk_start(blk);
-    const uint32_t done = (uint32_t)blk * kBlk;
-    const uint32_t target = live && vlen > done ? min((uint32_t)kBlk, vlen - done) : 0u;
-    uint16_t* const tlim = dw.tile + lane * kTP4 + target;
+    const uint32_t done = (uint32_t)blk * BLK;
+    const uint32_t target = live && vlen > done ? min((uint32_t)BLK, vlen - done) : 0u;
+    uint16_t* const tlim = dw.tile + lane * TP + target;
     auto quarter = [&]() {
       BPROF(pc[8] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(tp < tlim && !(pos8 < rdy)));
             pc[9] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(tp < tlim));)
@@ -1737,10 +1856,10 @@ __device__ __forceinline__ void decode_chunks4(const hfd::Tab4& tb, const hfd::D
     BPROF(tk = __builtin_readcyclecounter(); pc[3] += tk - tp0; tp0 = tk;)
     // symbols decoded past the block end move to its front; they are held in registers across
     // the reconstruction, which may use the tile as scratch
-    uint32_t* rw = reinterpret_cast<uint32_t*>(dw.tile + lane * kTP4);
+    uint32_t* rw = reinterpret_cast<uint32_t*>(dw.tile + lane * TP);
     uint32_t ovs[kF + 1];
 #pragma unroll
-    for (int i = 0; i <= kF; i++) ovs[i] = rw[kBlk / 2 + i];
+    for (int i = 0; i <= kF; i++) ovs[i] = rw[BLK / 2 + i];
     recon(blk);
     hfd::wave_sync();
 #pragma unroll
@@ -1748,14 +1867,33 @@ __device__ __forceinline__ void decode_chunks4(const hfd::Tab4& tb, const hfd::D
     hfd::wave_sync();
     // next block's columns; a lane that stopped short of the block (a dead or short chunk)
     // restarts at column 0, where its (zero) target keeps it out of the quarters
-    uint16_t* const row = dw.tile + lane * kTP4;
-    tp = tp >= row + kBlk ? tp - kBlk : row;
+    uint16_t* const row = dw.tile + lane * TP;
+    tp = tp >= row + BLK ? tp - BLK : row;
     BPROF(tk = __builtin_readcyclecounter(); pc[4] += tk - tp0; tp0 = tk;)
   }
 }
 
-template <typename T, bool ZZ, bool BUF>
-__global__ void __launch_bounds__(64 * kDec4Waves)
+// Per block width: 64 columns (8 waves per CU, a 15 KB ring + tile per wave) or 32 columns (12
+// waves per CU in 11 KB each: 3 waves per SIMD on the same LDS, recon_block32).  The step's chain
+// of two LDS round trips bounds the loop, so a third wave per SIMD pays although a 512^3 field's
+// 8192 bricks then make 2.67 rounds: f32 decompress 255 -> 229 us (config 2).  f64 keeps 64
+// columns (at 32 its reconstruction spills 29-37 VGPRs).
+#ifndef CUSZ_AMD_DEC3_BLK
+#define CUSZ_AMD_DEC3_BLK 0  // 0: 32 for f32 fields of >= 12 bricks per CU, else 64
+#endif
+template <int BLK>
+struct Dec3Cfg {
+  static constexpr int TP = BLK + 10;  // 9 overshoot columns, odd dword pitch
+  static constexpr size_t kCells = kD4Tile + (size_t)64 * TP * 2;
+  static constexpr size_t kRows = kCells + (size_t)kCellCap * 4;
+  static constexpr size_t kWaveBytes = kRows + (size_t)(65 + 64) * 4;
+  static constexpr int kWaves = BLK == 64 ? kDec4Waves : 12;
+  static_assert(((TP / 2) & 1) == 1 && BLK + 2 * kF + 1 <= TP, "tile pitch");
+  static_assert(sizeof(hfd::Tab4) + kWaves * kWaveBytes <= 160 * 1024, "LDS");
+};
+
+template <typename T, bool ZZ, bool BUF, int BLK>
+__global__ void __launch_bounds__(64 * Dec3Cfg<BLK>::kWaves)
 k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const uint8_t* __restrict__ revbook,
                 int bklen, const uint32_t* __restrict__ par_nbit, const uint32_t* __restrict__ par_entry, T* out,
                 uint32_t lx, uint32_t ly, uint32_t lz, T ebx2, T r, uint32_t nbx, uint32_t nby, uint32_t nbricks,
@@ -1764,10 +1902,11 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
   __shared__ hfd::Tab4 tb;  // static: table addresses fold into the ds offsets
   extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* wbase = dsm + (size_t)wid * kD4WaveBytes;
+  typedef Dec3Cfg<BLK> C;
+  uint8_t* wbase = dsm + (size_t)wid * C::kWaveBytes;
   uint16_t* tile = reinterpret_cast<uint16_t*>(wbase + kD4Tile);
-  uint32_t* cval = reinterpret_cast<uint32_t*>(wbase + kD4Cells);
-  BrickCells bc{cval, 1, reinterpret_cast<uint32_t*>(wbase + kD4Rows), reinterpret_cast<uint32_t*>(wbase + kD4Rows) + 65};
+  uint32_t* cval = reinterpret_cast<uint32_t*>(wbase + C::kCells);
+  BrickCells bc{cval, 1, reinterpret_cast<uint32_t*>(wbase + C::kRows), reinterpret_cast<uint32_t*>(wbase + C::kRows) + 65};
   const bool ranked = !ZZ && (ol.ncell == 0 || *ol.unsorted != ol.epoch);
   const DecWave4 dw{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(bitstream), 0, (int)(bs_words * 4u), (int)kBufRsrcW3),
                     reinterpret_cast<uint32_t*>(wbase) + lane, tile, (uint32_t)bklen, lane};
@@ -1812,7 +1951,9 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
   // bitstream lines in one L2), unless the field has fewer bricks than waves (a small slab): then
   // wave w of every workgroup takes brick w * grid + block, spreading them over every CU (one per
   // SIMD for 1024 bricks) instead of filling half the CUs two waves per SIMD
-  const uint32_t b0 = nbricks <= nw ? (uint32_t)wid * gridDim.x + blockIdx.x : blockIdx.x * (blockDim.x >> 6) + wid;
+  // (32-column blocks: always wave-major, so that the bricks' last, partial round is spread over
+  // every CU instead of ending on the first 170)
+  const uint32_t b0 = BLK == 32 || nbricks <= nw ? (uint32_t)wid * gridDim.x + blockIdx.x : blockIdx.x * (blockDim.x >> 6) + wid;
   Next nx = fetch(b0);  // (lands while the tables are built)
   hfd::build_tab4(tb, revbook, bklen);
   const hfd::DecRegs4 rg = hfd::load_dec_regs4(tb);
@@ -1853,18 +1994,26 @@ k_brick3_decode(const uint32_t* __restrict__ bitstream, uint32_t bs_words, const
       bc.vstride = nc <= kCellCap ? 1u : 2u;
     };
     auto recon = [&](int blk) {
-      if (blk == (int)(W / kBlk) - 1) prefetch(nx);  // the next brick (fetched during this block)
+      if (blk == (int)(W / BLK) - 1) prefetch(nx);  // the next brick (fetched during this block)
       const uint32_t nyv = min(8u, ly - y0), nzv = min(8u, lz - z0);
-      const size_t base_elem = (size_t)z0 * plane + (size_t)y0 * lx + (size_t)bx * W + (size_t)blk * kBlk;
-      if (ranked)
-        recon_block<T, ZZ, BUF, kTP4, true>(tile, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane, &bc);
-      else
-        recon_block<T, ZZ, BUF, kTP4, false>(tile, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane);
+      const size_t base_elem = (size_t)z0 * plane + (size_t)y0 * lx + (size_t)bx * W + (size_t)blk * BLK;
+      if constexpr (BLK == 64) {
+        if (ranked)
+          recon_block<T, ZZ, BUF, C::TP, true>(tile, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane, &bc);
+        else
+          recon_block<T, ZZ, BUF, C::TP, false>(tile, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane);
+      }
+      else {
+        if (ranked)
+          recon_block32<T, ZZ, BUF, C::TP, true>(tile, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane, &bc);
+        else
+          recon_block32<T, ZZ, BUF, C::TP, false>(tile, out, plane, lx, nyv, nzv, base_elem, r, ebx2, lane);
+      }
     };
     auto blk_start = [&](int blk) {
-      if (blk == (int)(W / kBlk) - 1) nx = fetch(brick + nw);
+      if (blk == (int)(W / BLK) - 1) nx = fetch(brick + nw);
     };
-    decode_chunks4(tb, rg, dw, live, vbase, nbit, W, pro, blk_start, recon BPROF_A4, W, f2);
+    decode_chunks4<BLK, C::TP>(tb, rg, dw, live, vbase, nbit, W, pro, blk_start, recon BPROF_A4, W, f2);
   }
 #ifdef CUSZ_AMD_DEC_PROFILE
   if (lane == 0)
@@ -3047,18 +3196,32 @@ int launch_brick_decode(const BrickLaunch& L, const uint32_t* bitstream, size_t 
   const size_t plane = (size_t)L.lx * L.ly;
   const bool buf = (7 * plane + 7 * (size_t)L.lx + (size_t)kBlk) * sizeof(T) < (1ull << 31);
   const uint32_t bw = (uint32_t)bs_words;
-  const size_t lds = (size_t)kDec4Waves * kD4WaveBytes;  // dynamic part
+  // 32-column blocks pay once the bricks fill the 12-wave slots (a 512^3 field); a small slab,
+  // one brick per wave, is bound by one brick's latency, which the 64-column blocks keep shorter
+  // (512 x 512 x 64: 88 against 94 us)
+  const bool b32 = CUSZ_AMD_DEC3_BLK ? CUSZ_AMD_DEC3_BLK == 32
+                                     : sizeof(T) == 4 && g.nbricks >= (uint32_t)Dec3Cfg<32>::kWaves * (uint32_t)L.ncu;
+  auto launch = [&](auto blk) {
+    constexpr int B3 = decltype(blk)::value;
+    const size_t lds = (size_t)Dec3Cfg<B3>::kWaves * Dec3Cfg<B3>::kWaveBytes;  // dynamic part
 #define DEC_LAUNCH(ZZ, BUF)                                                                                     \
-  k_brick3_decode<T, ZZ, BUF><<<L.ncu, 64 * kDec4Waves, lds, st>>>(bitstream, bw, revbook, bklen, par_nbit, par_entry, \
-                                                                  out, L.lx, L.ly, L.lz, ebx2, r, g.nbx, g.nby,       \
-                                                                  g.nbricks, ol)
-  if (zz) {
-    if (buf) DEC_LAUNCH(true, true); else DEC_LAUNCH(true, false);
-  }
-  else {
-    if (buf) DEC_LAUNCH(false, true); else DEC_LAUNCH(false, false);
-  }
+    k_brick3_decode<T, ZZ, BUF, B3><<<L.ncu, 64 * Dec3Cfg<B3>::kWaves, lds, st>>>(bitstream, bw, revbook, bklen, par_nbit, \
+                                                                              par_entry, out, L.lx, L.ly, L.lz, ebx2, r, \
+                                                                              g.nbx, g.nby, g.nbricks, ol)
+    if (zz) {
+      if (buf) DEC_LAUNCH(true, true); else DEC_LAUNCH(true, false);
+    }
+    else {
+      if (buf) DEC_LAUNCH(false, true); else DEC_LAUNCH(false, false);
+    }
 #undef DEC_LAUNCH
+  };
+  if constexpr (sizeof(T) == 4) {
+    if (b32) launch(std::integral_constant<int, 32>{});
+    else launch(std::integral_constant<int, 64>{});
+  }
+  else
+    launch(std::integral_constant<int, 64>{});
   return (int)hipGetLastError();
 }
 
