@@ -500,13 +500,16 @@ k_brick1_scan(const T* __restrict__ in, size_t n, T ebx2_r, T r, OutlierSink ol,
   constexpr int D = kScanAhead<T>;
   constexpr uint32_t kBE = 64 * 64 * V;  // elements per brick
   const uint32_t x0 = (uint32_t)lane * V;
-  auto issue_row = [&](uint32_t b, int row, T (&dst)[V]) {
-    // past the last brick: brick 0 with an empty range (reads 0, touches no memory): every path
-    // issues the same loads, so the waits can be counted (StepLoader::issue_row)
+  // a brick's descriptor, made once per brick (past the last brick: brick 0 with an empty range,
+  // which reads 0 and touches no memory, so every path issues the same loads and the waits can
+  // be counted, StepLoader::issue_row)
+  auto rows_of = [&](uint32_t b) {
     const bool live = b < nbricks;
     const size_t o = live ? (size_t)b * kBE : 0;
     const uint32_t span = live ? (uint32_t)(min((size_t)kBE, n - o) * sizeof(T)) : 0u;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(in + o), 0, (int)span, 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(in + o), 0, (int)span, 0x00020000);
+  };
+  auto issue_row = [&](__amdgpu_buffer_rsrc_t rs, int row, T (&dst)[V]) {
     const uint32_t off = ((uint32_t)row * (64 * V) + x0) * (uint32_t)sizeof(T);
 #pragma unroll
     for (int h = 0; h < (int)(V * sizeof(T) / 16); h++) {
@@ -543,9 +546,10 @@ k_brick1_scan(const T* __restrict__ in, size_t n, T ebx2_r, T r, OutlierSink ol,
   {
     const uint32_t u0 = it < nbricks ? pass1_brick(it, sp) : nbricks;
     if constexpr (ND == 2) cursor_at(u0, xi, yi);
+    const __amdgpu_buffer_rsrc_t r0s = rows_of(u0);
 #pragma unroll
     for (int j = 0; j < D; j++) {
-      issue_row(u0, j, q[j]);
+      issue_row(r0s, j, q[j]);
       if constexpr (ND == 2) {
         issue_north(u0, xi, yi, qn[j]);
         advance(xi, yi);
@@ -574,8 +578,13 @@ k_brick1_scan(const T* __restrict__ in, size_t n, T ebx2_r, T r, OutlierSink ol,
         carry = a;
       }
     }
+    const __amdgpu_buffer_rsrc_t rc = rows_of(u), rn = rows_of(un);
+    static_assert(64 % D == 0, "the rows ahead of a D-row block lie in one brick");
 #pragma unroll 1
-    for (int r0 = 0; r0 < 64; r0 += D)
+    for (int r0 = 0; r0 < 64; r0 += D) {
+      const bool tail = r0 + D >= 64;  // the rows ahead are the next brick's first rows
+      const __amdgpu_buffer_rsrc_t ahead = tail ? rn : rc;
+      const int ra = tail ? r0 + D - 64 : r0 + D;
 #pragma unroll
       for (int j = 0; j < D; j++) {
         const int row = r0 + j;
@@ -587,8 +596,7 @@ k_brick1_scan(const T* __restrict__ in, size_t n, T ebx2_r, T r, OutlierSink ol,
           for (int k = 0; k < V; k++) p[k] = p[k] - dround(qn[j][k] * ebx2_r);
         }
         const uint32_t bnext = row + D < 64 ? u : un;
-        if (row + D < 64) issue_row(u, row + D, q[j]);
-        else issue_row(un, row + D - 64, q[j]);
+        issue_row(ahead, ra + j, q[j]);
         if constexpr (ND == 2) {
           if (row + D == 64) cursor_at(un, xi, yi);  // the queue moves on to the next brick
           issue_north(bnext, xi, yi, qn[j]);
@@ -628,6 +636,7 @@ k_brick1_scan(const T* __restrict__ in, size_t n, T ebx2_r, T r, OutlierSink ol,
           emit_outliers<V>(ol, u, cnt, mask, olv, idx);
         }
       }
+    }
     finish_unit(ol, bcs, u, cnt, rowmask, s_hist, s_wg, bhist, hs, lane, sp, sp.hist && it < sp.count);
   }
   __syncthreads();
