@@ -128,6 +128,13 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} not built: run `make -C cusz_amd` (or __graft_entry__.build())")
+    # torch (the usual owner of the device buffers) first: its HIP runtime then serves the library
+    # too.  Loaded the other way round, the system runtime comes first and torch's device init
+    # later fails in that process ("No HIP GPUs are available").
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     P = C.c_void_p
     L.psz_create_resource_manager.restype = P

@@ -2,6 +2,7 @@
 import ctypes as C
 
 import numpy as np
+import torch  # noqa: F401  (before any HIP runtime is loaded: see cusz_amd.lib)
 
 import cusz_amd as cz
 
