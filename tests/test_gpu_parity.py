@@ -248,6 +248,29 @@ def test_rel_mode(oracle):
     np.testing.assert_array_equal(d2h(r.internals().d_quant_codes, 2 * data.size, np.uint16), codes_o)
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("where", ["body", "body_end", "tail"])
+def test_rel_mode_extrema_regions(dtype, where):
+    """The extrema pass reads the field in 16-B groups (several per lane and iteration), then the
+    last elements one by one: a minimum and maximum placed in the body, at the end of the grouped
+    part and in the scalar tail must be found (extrema.cuhip.inl:86-208)."""
+    dims = (307, 125, 121)  # n % 16 == 15: a ragged group count and a scalar tail for f32 and f64
+    n = dims[0] * dims[1] * dims[2]
+    e = 16 // np.dtype(dtype).itemsize
+    groups = n // e
+    assert groups % 4 and n % e
+    data = (np.sin(np.arange(n) * 1e-3) * 5.0).astype(dtype)
+    pos = {"body": (groups // 2) * e + 1, "body_end": (groups // 4 * 4) * e + 1, "tail": n - 1}[where]
+    data[pos] = 40.0
+    data[pos - 1] = -30.0
+    r = cz.Resource(cz.F4 if dtype == np.float32 else cz.F8, dims)
+    d_in = to_device(data)
+    r.compress(d_in.data_ptr(), 1e-3, cz.Rel)
+    h = r.header
+    assert h.min_val == -30.0 and h.max_val == 40.0
+    r.close()
+
+
 @pytest.mark.parametrize("decoder", [cz.DECODER_WAVE, cz.DECODER_LANE, cz.DECODER_AUTO])
 def test_long_chunks_high_entropy_all_decoders(oracle, decoder):
     """sublen 8192 with ~10-bit codes: the wave decoder's LDS staging would exceed its budget,
